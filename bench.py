@@ -1,0 +1,269 @@
+"""bench.py -- device-resident N-K encode(+XXH64 of every part)+decode
+throughput on MI355X, one process per GPU, weak scaling over stripes.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Step = one pass of the hot path over one batch resident in HBM:
+  nkfs_nk8_encode  (fused encode + XXH64 of every part), then
+  nkfs_nk8_decode  (per-stripe K x K inverse + apply) from the seeded
+                   survivors (n-k parts erased per stripe).
+value = user bytes of all ranks x steps / max-over-ranks wall time (GiB/s).
+
+The dominant kernel's roofline is measured live with HIP events on the
+stream the library launches on (torch's current stream); algorithmic bytes
+per stripe are SURVEY.md §8(d)'s: encode+hash B + n*ps + 8n.  The CPU
+baseline (rank 0, N=1) times the reference's own code (oracle/_ref) on a
+bounded sample of the same workload on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident N-K encode+decode, 4KiB–1MiB stripes, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (stripes per GPU, block size, n, k, description)
+    "c2": (65536, 4096, 4, 2, "C2: N=4,K=2 encode(+XXH64/part)+decode(2 erased), 65536 x 4 KiB stripes per GPU"),
+    "c3": (2048, 1048576, 8, 5, "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 2048 x 1 MiB stripes per GPU"),
+    "c4": (16384, 262144, 8, 5, "C4: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 16384 x 256 KiB stripes per GPU"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pcie", action="store_true", help="also time the host-memory (PCIe-inclusive) path")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------ distributed
+
+def dist_setup(backend: str):
+    """(rank, world, local_rank); initialises torch.distributed when the
+    launcher set WORLD_SIZE > 1."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def stripe_range(rank: int, per_rank: int):
+    """Weak scaling: rank r owns stripes [r*per_rank, (r+1)*per_rank)."""
+    return rank * per_rank, per_rank
+
+
+def reduce_max(value: float, device) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_digest_xor(local_xor: int, device) -> list[int]:
+    """All-gather each rank's 64-bit xor-of-part-digests (the control
+    collective: 8 bytes per rank)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([local_xor - (1 << 64) if local_xor >= (1 << 63) else local_xor], dtype=torch.int64,
+                     device=device)
+    if not (dist.is_available() and dist.is_initialized()):
+        return [local_xor]
+    out = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, v)
+    return [int(x.item()) & 0xFFFFFFFFFFFFFFFF for x in out]
+
+
+def barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+# --------------------------------------------------------------- workload
+
+def main():
+    args = parse()
+    import torch
+
+    rank, world, local = dist_setup("nccl")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    os.environ["NKFS_DEVICE"] = str(local)
+
+    from nkfs_amd import _lib, batch, synth
+    L = _lib.lib()
+    _lib.check(L.nkfs_gpu_init(local), "nkfs_gpu_init")
+
+    S, B, n, k, desc = CONFIGS[args.config]
+    first, _ = stripe_range(rank, S)
+    ps = batch.part_size(B, k)
+    stream = torch.cuda.current_stream(device)
+
+    blocks = batch.synth(S, B, first=first, device=device)
+    ids_np = synth.batch_ids(S, n, first=first)
+    ids = torch.from_numpy(ids_np).to(device)
+    avail = torch.from_numpy(synth.batch_survivors(S, n, k, first=first)).to(device)
+    parts = torch.empty((S * n, batch.part_pitch(B, k)), dtype=torch.uint8, device=device)
+    digests = torch.empty(S * n, dtype=torch.int64, device=device)
+    out = torch.empty((S, B), dtype=torch.uint8, device=device)
+    work = batch.decode_workspace(S, k, device)
+    status = torch.empty(S, dtype=torch.int32, device=device)
+
+    def step():
+        batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream)
+        batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = reduce_max(t1 - t0, device)
+
+    # correctness of what was timed: decode == input, digests vs oracle sample
+    ok = bool(torch.equal(out, blocks[:, :B])) and int(status.abs().sum()) == 0
+    dig = [int(x) & 0xFFFFFFFFFFFFFFFF for x in digests.cpu().tolist()]
+    from oracle import oracle as O
+    blocks_np = blocks[:, :B].cpu().numpy()
+    for s in range(0, S, max(1, S // 64)):
+        want = [O.xxh64(p) for p in O.encode(blocks_np[s], n, k, ids_np[s])]
+        ok &= dig[s * n:(s + 1) * n] == want
+    dx = 0
+    for d in dig:
+        dx ^= d
+    gathered = gather_digest_xor(dx, device)
+
+    # dominant kernel: encode(+hash) alone, HIP events on the launch stream
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    reps = max(5, args.steps)
+    ev0.record(stream)
+    for _ in range(reps):
+        batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    enc_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    ev0.record(stream)
+    for _ in range(reps):
+        batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    dec_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    enc_bytes = S * (B + n * ps + 8 * n)
+    dec_bytes = S * (k * ps + B + k)
+
+    user_bytes = S * B * world * args.steps
+    value = user_bytes / elapsed / 2**30
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846)",
+        "config": {"workload": desc, "n": n, "k": k, "block_size": B, "stripes_per_gpu": S,
+                   "part_size": ps, "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "nkfs_nk8_encode (encode + XXH64 per part)",
+            "achieved": round(enc_bytes / enc_s / 1e9, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(enc_bytes / enc_s / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "bytes_per_launch": enc_bytes,
+            "us_per_launch": round(enc_s * 1e6, 2),
+        },
+        "decode": {"achieved_GBps": round(dec_bytes / dec_s / 1e9, 1), "us_per_launch": round(dec_s * 1e6, 2),
+                   "bytes_per_launch": dec_bytes},
+        "verified": ok,
+        "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(S, B, n, k, args.cpu_seconds)
+    if rank == 0 and args.pcie:
+        result["pcie_inclusive_GiBps"] = pcie_rate(batch, blocks_np, S, B, n, k, ids, avail, device, stream)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def cpu_baseline(S, B, n, k, target_s):
+    """The reference's own split + XXH64 + assemble (oracle/_ref), on a
+    bounded sample of this workload, on the host cores of this box."""
+    from nkfs_amd import synth
+    from oracle import oracle as O
+    kind = "reference" if O.ref_lib() is not None else "port"
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    probe = min(S, max(16, (1 << 22) // B))
+    blocks = synth.batch_bytes(probe, B)
+    sv = synth.batch_survivors(probe, n, k)
+    secs, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
+    count = int(min(S * 4, max(probe, probe * target_s / max(secs, 1e-6))))
+    count = max(threads, min(count, (2 << 30) // B))
+    blocks = synth.batch_bytes(count, B)
+    sv = synth.batch_survivors(count, n, k)
+    secs, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
+    return {"value": round(count * B / secs / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{count} stripes x {B} B (N={n},K={k}): nk8_split_block + XXH64 of every part + "
+                      f"nk8_assemble_block from {k} survivors, {threads} pthreads, {secs:.1f} s"}
+
+
+def pcie_rate(batch, blocks_np, S, B, n, k, ids, avail, device, stream):
+    """Host-memory path: pinned H2D of the blocks, encode+decode, D2H of the
+    parts and the digests (DESIGN.md records it; never the headline)."""
+    import torch
+    host_in = torch.from_numpy(blocks_np).pin_memory()
+    ps = batch.part_pitch(B, k)
+    host_parts = torch.empty((S * n, ps), dtype=torch.uint8).pin_memory()
+    dev_in = torch.empty((S, B), dtype=torch.uint8, device=device)
+    parts = torch.empty((S * n, ps), dtype=torch.uint8, device=device)
+    dig = torch.empty(S * n, dtype=torch.int64, device=device)
+    torch.cuda.synchronize(device)
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dev_in.copy_(host_in, non_blocking=True)
+        batch.encode(dev_in, B, n, k, ids, parts, dig, stream=stream)
+        host_parts.copy_(parts, non_blocking=True)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    return round(S * B * reps / (t1 - t0) / 2**30, 3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+/*
+ * nkfs_gpu.h -- batched, device-resident entry points of libnkfs_crt.so.
+ *
+ * The reference encodes one block per call with ids it draws itself
+ * (crt/nk8.c:344-444) and decodes one block per call (crt/nk8.c:446-599).
+ * On MI355X the same arithmetic runs over whole batches of independent
+ * stripes already resident in HBM, with the ids passed in explicitly so a
+ * batch is reproducible bit for bit.  All pointers named d_* are device
+ * pointers; `stream` is a hipStream_t (NULL = the default stream); calls are
+ * asynchronous on that stream and return 0 or a negative errno for argument
+ * errors (-EINVAL), calls before nk8_init/nkfs_gpu_init (-EAGAIN) and launch
+ * failures (-EIO).  No host synchronisation happens inside, so calls can be
+ * captured in a hipGraph.
+ *
+ * Layout (uniform batch of `nstripes` stripes):
+ *   block s        d_blocks + s*block_pitch, block_size bytes, interleaved
+ *                  (row j = bytes j*k .. j*k+k-1, crt/nk8.c:411)
+ *   part i of s    d_parts + (s*n + i)*part_pitch, part_size bytes (planar)
+ *   ids of s       d_ids + s*n, n bytes (evaluation point of part i)
+ *   digest (s,i)   d_digests[s*n + i] = XXH64(part, part_size, 0)
+ * part_pitch must be >= nkfs_part_size(block_size, k) and a multiple of 16.
+ */
+#ifndef NKFS_GPU_H
+#define NKFS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Initialise the GPU side without the reference's self test (nk8_init runs
+ * this plus the test).  device < 0: env NKFS_DEVICE or the current device. */
+int nkfs_gpu_init(int device);
+/* 1 when the library has a usable GPU context. */
+int nkfs_gpu_ready(void);
+
+/* ceil(block_size/k) -- crt/nk8.c:311-317. */
+uint32_t nkfs_part_size(uint32_t block_size, int k);
+/* part_size rounded up to 16 bytes: the pitch ragged batches use. */
+uint64_t nkfs_part_pitch(uint32_t block_size, int k);
+
+/* Encode (+ XXH64 of every part when d_digests != NULL) a uniform batch.
+ * Same parameter rules as nk8_split_block; ids must be nonzero. */
+int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch,
+		    uint32_t block_size, uint32_t nstripes, int n, int k,
+		    const uint8_t *d_ids, uint8_t *d_parts, uint64_t part_pitch,
+		    uint64_t *d_digests, void *stream);
+
+/* Ragged batch (stripes of different sizes): block s at
+ * d_blocks + d_block_off[s] with d_block_size[s] bytes; part i of s at
+ * d_parts + d_part_off[s] + i*nkfs_part_pitch(d_block_size[s], k).
+ * max_block_size bounds every d_block_size[s]. */
+int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
+			   const uint32_t *d_block_size, uint32_t max_block_size,
+			   uint32_t nstripes, int n, int k, const uint8_t *d_ids,
+			   uint8_t *d_parts, const uint64_t *d_part_off,
+			   uint64_t *d_digests, void *stream);
+
+/* Decode a uniform batch.  Parts live in slots laid out as the encoder's
+ * output (n_slots per stripe, pitch part_pitch); d_ids[s*n_slots + j] is the
+ * id of slot j.  d_avail[s*navail + c] lists the slots offered for stripe s
+ * in caller order; like nk8_assemble_block the first k with distinct ids
+ * are used.  d_work: nkfs_decode_workspace(nstripes, k) bytes of device
+ * scratch.  d_status[s] (may be NULL) receives 0 or -EINVAL (fewer than k
+ * distinct ids) per stripe; such stripes are left unwritten. */
+uint64_t nkfs_decode_workspace(uint32_t nstripes, int k);
+int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots,
+		    const uint8_t *d_ids, const uint8_t *d_avail, int navail,
+		    int k, uint32_t block_size, uint8_t *d_blocks,
+		    uint64_t block_pitch, uint32_t nstripes, void *d_work,
+		    int32_t *d_status, void *stream);
+
+/* XXH64 of `count` messages d_base + d_off[i], d_len[i] bytes each
+ * (d_off[i] a multiple of 8) -- the batched form of csum_* for the core's
+ * per-64 KiB-block integrity sums (core/dio.c:26-37). */
+int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off,
+		     const uint64_t *d_len, uint32_t count, uint64_t seed,
+		     uint64_t *d_out, void *stream);
+
+/* Fill a uniform batch with the seeded counter-based splitmix64 stripes of
+ * nkfs_amd/synth.py (bench / test input synthesis on the device). */
+int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch,
+		      uint32_t block_size, uint32_t nstripes, uint64_t seed,
+		      uint64_t first_stripe, void *stream);
+
+/* Device memory helpers for callers without their own allocator. */
+void *nkfs_dev_alloc(size_t bytes);
+void nkfs_dev_free(void *d_ptr);
+int nkfs_memcpy_h2d(void *d_dst, const void *src, size_t bytes);
+int nkfs_memcpy_d2h(void *dst, const void *d_src, size_t bytes);
+int nkfs_stream_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

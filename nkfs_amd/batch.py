@@ -1,0 +1,127 @@
+"""Device-resident batch API over torch tensors (include/nkfs_gpu.h).
+
+torch is only the allocator and stream provider here: every computation is
+a HIP kernel inside libnkfs_crt.so, launched on torch's current stream.
+
+Layout of a uniform batch (see include/nkfs_gpu.h):
+    blocks  uint8 [nstripes, block_pitch]     interleaved user data
+    ids     uint8 [nstripes, n]               part evaluation points
+    parts   uint8 [nstripes * n, part_pitch]  planar parts
+    digests int64 [nstripes * n]              XXH64(part) (seed 0)
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import check, lib
+
+U8 = torch.uint8
+
+
+def gpu_init(device: int = -1) -> None:
+    check(lib().nkfs_gpu_init(device), "nkfs_gpu_init")
+
+
+def part_size(block_size: int, k: int) -> int:
+    return int(lib().nkfs_part_size(block_size, k))
+
+
+def part_pitch(block_size: int, k: int) -> int:
+    return int(lib().nkfs_part_pitch(block_size, k))
+
+
+def _stream(stream) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _need(t, dtype, name):
+    if not (t.is_cuda and t.dtype == dtype and t.is_contiguous()):
+        raise ValueError(f"{name}: expected a contiguous {dtype} CUDA tensor")
+
+
+def encode(blocks: torch.Tensor, block_size: int, n: int, k: int, ids: torch.Tensor,
+           parts: torch.Tensor | None = None, digests: bool | torch.Tensor = True, stream=None):
+    """Encode (+ XXH64 of every part).  Returns (parts, digests|None)."""
+    _need(blocks, U8, "blocks")
+    _need(ids, U8, "ids")
+    nstripes = blocks.shape[0]
+    pitch = part_pitch(block_size, k)
+    if parts is None:
+        parts = torch.empty((nstripes * n, pitch), dtype=U8, device=blocks.device)
+    _need(parts, U8, "parts")
+    if digests is True:
+        digests = torch.empty(nstripes * n, dtype=torch.int64, device=blocks.device)
+    elif digests is False:
+        digests = None
+    check(lib().nkfs_nk8_encode(blocks.data_ptr(), blocks.stride(0) if blocks.dim() > 1 else block_size,
+                                block_size, nstripes, n, k, ids.data_ptr(), parts.data_ptr(),
+                                parts.stride(0), _ptr(digests), _stream(stream)), "nkfs_nk8_encode")
+    return parts, digests
+
+
+def encode_ragged(blocks: torch.Tensor, block_off: torch.Tensor, block_sizes: torch.Tensor, n: int, k: int,
+                  ids: torch.Tensor, parts: torch.Tensor, part_off: torch.Tensor,
+                  digests: torch.Tensor | None, max_block_size: int, stream=None):
+    for t, dt, nm in ((blocks, U8, "blocks"), (block_off, torch.int64, "block_off"),
+                      (block_sizes, torch.int32, "block_sizes"), (ids, U8, "ids"), (parts, U8, "parts"),
+                      (part_off, torch.int64, "part_off")):
+        _need(t, dt, nm)
+    check(lib().nkfs_nk8_encode_ragged(blocks.data_ptr(), block_off.data_ptr(), block_sizes.data_ptr(),
+                                       max_block_size, block_sizes.numel(), n, k, ids.data_ptr(),
+                                       parts.data_ptr(), part_off.data_ptr(), _ptr(digests), _stream(stream)),
+          "nkfs_nk8_encode_ragged")
+
+
+def decode_workspace(nstripes: int, k: int, device) -> torch.Tensor:
+    return torch.empty(max(int(lib().nkfs_decode_workspace(nstripes, k)), 1), dtype=U8, device=device)
+
+
+def decode(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Tensor, k: int, block_size: int,
+           out: torch.Tensor | None = None, work: torch.Tensor | None = None,
+           status: torch.Tensor | None = None, stream=None):
+    """Decode every stripe from the slots listed in avail[s] (first k with
+    distinct ids).  Returns (blocks [nstripes, block_size], status int32)."""
+    _need(parts, U8, "parts")
+    _need(ids, U8, "ids")
+    _need(avail, U8, "avail")
+    nstripes = avail.shape[0]
+    navail = avail.shape[1]
+    dev = parts.device
+    if out is None:
+        out = torch.empty((nstripes, block_size), dtype=U8, device=dev)
+    if work is None:
+        work = decode_workspace(nstripes, k, dev)
+    if status is None:
+        status = torch.empty(nstripes, dtype=torch.int32, device=dev)
+    check(lib().nkfs_nk8_decode(parts.data_ptr(), parts.stride(0), n_slots, ids.data_ptr(), avail.data_ptr(),
+                                navail, k, block_size, out.data_ptr(), out.stride(0) if out.dim() > 1 else block_size,
+                                nstripes, work.data_ptr(), status.data_ptr(), _stream(stream)), "nkfs_nk8_decode")
+    return out, status
+
+
+def xxh64_batch(base: torch.Tensor, off: torch.Tensor, lens: torch.Tensor, seed: int = 0, stream=None):
+    _need(base, U8, "base")
+    out = torch.empty(off.numel(), dtype=torch.int64, device=base.device)
+    check(lib().nkfs_xxh64_batch(base.data_ptr(), off.data_ptr(), lens.data_ptr(), off.numel(), seed,
+                                 out.data_ptr(), _stream(stream)), "nkfs_xxh64_batch")
+    return out
+
+
+def synth(nstripes: int, block_size: int, pitch: int | None = None, seed: int | None = None, first: int = 0,
+          device="cuda", stream=None) -> torch.Tensor:
+    from .synth import SEED
+    pitch = pitch or ((block_size + 15) // 16) * 16
+    t = torch.empty((nstripes, pitch), dtype=U8, device=device)
+    check(lib().nkfs_synth_blocks(t.data_ptr(), pitch, block_size, nstripes, SEED if seed is None else seed,
+                                  first, _stream(stream)), "nkfs_synth_blocks")
+    return t
+
+
+def digests_u64(d: torch.Tensor):
+    """int64 digest tensor -> list of Python unsigned ints."""
+    return [v & 0xFFFFFFFFFFFFFFFF for v in d.cpu().tolist()]

@@ -1,0 +1,481 @@
+// nk8_kernels.hip -- gfx950 kernels for the nkfs N-K erasure code and its
+// per-part XXH64 (reference: irqlevel/nkfs crt/nk8.c, crt/xxhash.c).
+//
+// Kernels in this file are the general path: any (n, k) the reference
+// accepts (2<=k<=n<=255, k<=254), any block size, uniform or ragged
+// batches.  The streaming fast path for n <= 8 (fused encode + XXH64 with
+// per-stripe packed product tables in LDS) lives in nk8_fast.hip and is
+// preferred by the dispatch in nkfs_launch_encode when it applies.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include "gf256.h"
+#include "nkfs_internal.h"
+#include "xxh64_dev.h"
+
+using namespace nkfs;
+typedef uint8_t u8;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+namespace {
+
+__host__ __device__ inline u32 part_size_of(u32 block_size, int k)
+{
+    return block_size / u32(k) + ((block_size % u32(k)) ? 1u : 0u);
+}
+
+__host__ __device__ inline u64 pitch_of(u32 block_size, int k)
+{
+    return (u64(part_size_of(block_size, k)) + 15) & ~u64(15);
+}
+
+struct StripeView {
+    const u8 *blk;
+    u8 *parts;
+    u64 pitch;
+    u32 B;
+    u32 ps;
+};
+
+__device__ inline StripeView stripe_view(const nkfs_geom &g, u32 s)
+{
+    StripeView v;
+    if (g.block_sizes) {
+        v.B = g.block_sizes[s];
+        v.blk = g.blocks + g.block_off[s];
+        v.parts = g.parts + g.part_off[s];
+        v.pitch = pitch_of(v.B, g.k);
+    } else {
+        v.B = g.block_size;
+        v.blk = g.blocks + u64(s) * g.block_pitch;
+        v.parts = g.parts + u64(s) * u64(g.n) * g.part_pitch;
+        v.pitch = g.part_pitch;
+    }
+    v.ps = part_size_of(v.B, g.k);
+    return v;
+}
+
+// GF(2^8) log/antilog in LDS.
+struct GfLds {
+    uint16_t log[256];
+    u8 exp[768];
+};
+
+__device__ inline void gf_stage(GfLds &L, const GfTables *g)
+{
+    for (int i = threadIdx.x; i < 256; i += blockDim.x)
+        L.log[i] = g->log[i];
+    for (int i = threadIdx.x; i < 768; i += blockDim.x)
+        L.exp[i] = g->exp[i];
+    __syncthreads();
+}
+
+__device__ inline u8 gf_mul(const GfLds &L, u8 a, u8 b)
+{
+    return (a && b) ? L.exp[L.log[a] + L.log[b]] : u8(0);
+}
+
+__device__ inline u8 gf_div(const GfLds &L, u8 a, u8 b)
+{
+    return (a && b) ? L.exp[L.log[a] + 255 - L.log[b]] : u8(0);
+}
+
+__device__ inline u64 shfl64(u64 v, int src)
+{
+    u32 lo = __shfl(u32(v), src, 64);
+    u32 hi = __shfl(u32(v >> 32), src, 64);
+    return (u64(hi) << 32) | lo;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------- GF tables
+
+__global__ void k_gf_init(GfTables *t)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0)
+        return;
+    u8 x = 1;
+    for (int i = 0; i < 255; ++i) {
+        t->exp[i] = x;
+        t->exp[i + 255] = x;
+        t->log[x] = uint16_t(i);
+        x = gf_mul_slow(x, 3);
+    }
+    for (int i = 510; i < 768; ++i)
+        t->exp[i] = 0;
+    t->log[0] = LOG_ZERO;
+}
+
+// ------------------------------------------------------ generic encode
+//
+// grid (nstripes, ceil(max_ps / 256)); one thread per row j of stripe
+// blockIdx.x, computing byte j of every part:
+//   part_i[j] = XOR_m ids[i]^m * d[j*k + m]     (crt/nk8.c:403-420)
+// with d zero beyond block_size (the reference's padded tail row).
+__global__ __launch_bounds__(256) void k_encode_generic(nkfs_geom g, const u8 *ids, const GfTables *gft)
+{
+    __shared__ GfLds L;
+    __shared__ uint16_t lid[256];
+    gf_stage(L, gft);
+    const u32 s = blockIdx.x;
+    const StripeView v = stripe_view(g, s);
+    for (int i = threadIdx.x; i < g.n; i += blockDim.x)
+        lid[i] = L.log[ids[u64(s) * g.n + i]];
+    __syncthreads();
+    const u32 j = blockIdx.y * blockDim.x + threadIdx.x;
+    if (j >= v.ps)
+        return;
+    const u64 row = u64(j) * g.k;
+    const int kk = g.k;
+    for (int i = 0; i < g.n; ++i) {
+        const int li = lid[i];
+        int la = 0;  // log of ids[i]^m
+        u8 acc = 0;
+        for (int m = 0; m < kk; ++m) {
+            const u64 pos = row + m;
+            const u8 x = pos < v.B ? v.blk[pos] : u8(0);
+            if (x)
+                acc ^= L.exp[la + L.log[x]];
+            la += li;
+            if (la >= 255)
+                la -= 255;
+        }
+        v.parts[u64(i) * v.pitch + j] = acc;
+    }
+}
+
+// ---------------------------------------------------- XXH64 over parts
+//
+// Four lanes per part (accumulator a = lane & 3 consumes words a, a+4, ...),
+// converge + tail + avalanche in lane a == 0.  Part bases are 16-byte
+// aligned (pitch is a multiple of 16).
+__global__ __launch_bounds__(256) void k_hash_parts(nkfs_geom g, u64 *digests)
+{
+    const u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x;
+    const u64 msg = t >> 2;
+    const int a = int(t & 3);
+    const u64 total = u64(g.nstripes) * u64(g.n);
+    const bool live = msg < total;
+    const u8 *p = nullptr;
+    u32 len = 0;
+    if (live) {
+        const u32 s = u32(msg / u32(g.n));
+        const u32 i = u32(msg % u32(g.n));
+        const StripeView v = stripe_view(g, s);
+        p = v.parts + u64(i) * v.pitch;
+        len = v.ps;
+    }
+    u64 acc = xxh_acc_init(a, 0);
+    const u32 nst = len >> 5;
+    const u64 *w = reinterpret_cast<const u64 *>(p) + a;
+    for (u32 r = 0; r < nst; ++r)
+        acc = xxh_round(acc, w[4 * r]);
+    const int base = int(threadIdx.x & 63) & ~3;
+    const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+    const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+    if (!live || a != 0)
+        return;
+    u64 h = len >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+    h += len;
+    digests[msg] = xxh_tail(h, p + (u64(nst) << 5), len & 31);
+}
+
+// Same, for an arbitrary message list (offsets multiple of 8).
+__global__ __launch_bounds__(256) void k_xxh64_batch(const u8 *base, const u64 *off, const u64 *lenv,
+                                                     u32 count, u64 seed, u64 *out)
+{
+    const u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x;
+    const u64 msg = t >> 2;
+    const int a = int(t & 3);
+    const bool live = msg < count;
+    const u8 *p = live ? base + off[msg] : nullptr;
+    const u64 len = live ? lenv[msg] : 0;
+    u64 acc = xxh_acc_init(a, seed);
+    const u64 nst = len >> 5;
+    const u64 *w = reinterpret_cast<const u64 *>(p) + a;
+    for (u64 r = 0; r < nst; ++r)
+        acc = xxh_round(acc, w[4 * r]);
+    const int b = int(threadIdx.x & 63) & ~3;
+    const u64 v1 = shfl64(acc, b), v2 = shfl64(acc, b + 1);
+    const u64 v3 = shfl64(acc, b + 2), v4 = shfl64(acc, b + 3);
+    if (!live || a != 0)
+        return;
+    u64 h = len >= 32 ? xxh_converge(v1, v2, v3, v4) : seed + XP5;
+    h += len;
+    out[msg] = xxh_tail(h, p + (nst << 5), u32(len & 31));
+}
+
+// Streaming XXH64 for the csum_*/XXH64_* compatibility entry points: fold
+// `nst` whole 32-byte stripes into the four accumulators of one state
+// (crt/xxhash.c:788-821), then (separately) finish.
+__global__ void k_xxh64_stripes(u64 *state_v, const u8 *data, u64 nst)
+{
+    const int a = threadIdx.x;
+    if (a >= 4)
+        return;
+    u64 acc = state_v[a];
+    const u64 *w = reinterpret_cast<const u64 *>(data) + a;
+    for (u64 r = 0; r < nst; ++r)
+        acc = xxh_round(acc, w[4 * r]);
+    state_v[a] = acc;
+}
+
+__global__ void k_xxh64_finish(u64 *out, const u64 *state_v, u64 total_len, u64 seed, const u8 *tail,
+                               u32 tail_len)
+{
+    if (threadIdx.x != 0)
+        return;
+    u64 h = total_len >= 32 ? xxh_converge(state_v[0], state_v[1], state_v[2], state_v[3]) : seed + XP5;
+    h += total_len;
+    *out = xxh_tail(h, tail, tail_len);
+}
+
+// ------------------------------------------------------------- decode
+//
+// Per stripe: pick the first k offered parts with distinct ids
+// (crt/nk8.c:512-537), then W = V^-1 for V[m][c] = x_c^m (crt/nk8.c:509-546).
+// W is computed in closed form: column c of the decode is the Lagrange basis
+// polynomial L_c(t) = prod_{c' != c} (t + x_c') / (x_c + x_c'), so
+// W[c][m] = [t^m] L_c(t).  The inverse of a matrix is unique, so this is
+// bit-identical to the reference's Gauss-Jordan (checked against the oracle
+// and the golden fixtures); it costs O(k^2) per stripe instead of O(k^3)
+// and spreads over one thread per column.
+// work per stripe: k bytes of slot index, then W row-major (k*k bytes).
+__global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *avail, int n_slots, int navail,
+                                                    int k, u8 *work, int32_t *status, const GfTables *gft)
+{
+    __shared__ GfLds L;
+    __shared__ u8 x[256], slot[256], M[256];
+    __shared__ int have;
+    gf_stage(L, gft);
+    const u32 s = blockIdx.x;
+    u8 *wk = work + u64(s) * u64(k + k * k);
+    if (threadIdx.x == 0) {
+        const u8 *sid = ids + u64(s) * n_slots;
+        const u8 *sav = avail + u64(s) * navail;
+        int h = 0;
+        for (int c = 0; c < navail && h < k; ++c) {
+            const u8 sl = sav[c];
+            const u8 id = sid[sl];
+            bool dup = false;
+            for (int d = 0; d < c; ++d)
+                dup |= sid[sav[d]] == id;
+            if (dup)
+                continue;
+            x[h] = id;
+            slot[h] = sl;
+            ++h;
+        }
+        have = h;
+        if (status)
+            status[s] = h < k ? -EINVAL : 0;
+        if (h == k) {
+            // M(t) = prod_c (t + x_c), coefficients M[0..k]
+            M[0] = 1;
+            for (int c = 0; c < k; ++c) {
+                M[c + 1] = M[c];
+                for (int i = c; i >= 1; --i)
+                    M[i] = M[i - 1] ^ gf_mul(L, x[c], M[i]);
+                M[0] = gf_mul(L, x[c], M[0]);
+            }
+        }
+    }
+    __syncthreads();
+    if (have < k)
+        return;
+    for (int c = threadIdx.x; c < k; c += blockDim.x) {
+        wk[c] = slot[c];
+        u8 *row = wk + k + c * k;
+        const u8 xc = x[c];
+        // Q(t) = M(t) / (t + x_c), synthetic division from the top.
+        u8 q = M[k];
+        row[k - 1] = q;
+        for (int i = k - 1; i >= 1; --i) {
+            q = M[i] ^ gf_mul(L, xc, q);
+            row[i - 1] = q;
+        }
+        // D = Q(x_c) = prod_{c' != c} (x_c + x_c')
+        u8 d = 0;
+        for (int i = k - 1; i >= 0; --i)
+            d = gf_mul(L, d, xc) ^ row[i];
+        for (int i = 0; i < k; ++i)
+            row[i] = gf_div(L, row[i], d);
+    }
+}
+
+// grid (nstripes, ceil(ps/256)); thread = row j:
+//   block[j*k + m] = XOR_c part_c[j] * W[c][m]        (crt/nk8.c:552-582)
+// only bytes below block_size are written (the tail row's padding is not).
+__global__ __launch_bounds__(256) void k_decode_generic(nkfs_geom g, int n_slots, const u8 *work,
+                                                        const int32_t *status, const GfTables *gft)
+{
+    __shared__ GfLds L;
+    gf_stage(L, gft);
+    const u32 s = blockIdx.x;
+    if (status && status[s])
+        return;
+    const int k = g.k;
+    const u32 B = g.block_size;
+    const u32 ps = part_size_of(B, k);
+    const u32 j = blockIdx.y * blockDim.x + threadIdx.x;
+    if (j >= ps)
+        return;
+    const u8 *wk = work + u64(s) * u64(k + k * k);
+    const u8 *sparts = g.parts + u64(s) * u64(n_slots) * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+    const u64 row = u64(j) * k;
+    for (int m = 0; m < k; ++m) {
+        if (row + m >= B)
+            break;
+        u8 acc = 0;
+        for (int c = 0; c < k; ++c) {
+            const u8 pv = sparts[u64(wk[c]) * g.part_pitch + j];
+            acc ^= gf_mul(L, pv, wk[k + c * k + m]);
+        }
+        out[row + m] = acc;
+    }
+}
+
+// ---------------------------------------------------------- synthetic
+// word(seed, s, w) = mix64(seed + GAMMA*((s << 32) + w + 1)) -- synth.py.
+__device__ inline u64 mix64(u64 z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth(u8 *blocks, u64 pitch, u32 B, u32 nstripes, u64 seed, u64 first)
+{
+    const u32 nw = (B + 7) / 8;
+    const u64 total = u64(nw) * nstripes;
+    for (u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += u64(gridDim.x) * blockDim.x) {
+        const u64 s = t / nw, w = t % nw;
+        const u64 val = mix64(seed + 0x9E3779B97F4A7C15ull * (((first + s) << 32) + w + 1));
+        u8 *dst = blocks + s * pitch + w * 8;
+        if (w * 8 + 8 <= B) {
+            if ((reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+                *reinterpret_cast<u64 *>(dst) = val;
+                continue;
+            }
+        }
+        for (u32 b = 0; b < 8 && w * 8 + b < B; ++b)
+            dst[b] = u8(val >> (8 * b));
+    }
+}
+
+// ----------------------------------------------------------- launchers
+
+extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, const void *gf, hipStream_t st);
+
+static int launch_ok(void)
+{
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -EIO;
+}
+
+static u32 max_part_size(const nkfs_geom *g, u32 max_block)
+{
+    return part_size_of(g->block_sizes ? max_block : g->block_size, g->k);
+}
+
+extern "C" size_t nkfs_gf_tables_bytes(void) { return sizeof(GfTables); }
+
+extern "C" uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k)
+{
+    return u64(nstripes) * u64(k + k * k);
+}
+
+extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
+{
+    hipLaunchKernelGGL(k_gf_init, dim3(1), dim3(64), 0, (hipStream_t)stream, (GfTables *)gf);
+    return launch_ok();
+}
+
+// ragged batches pass the bound on block sizes in g->block_size
+extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
+                                  void *stream)
+{
+    if (!g->nstripes)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;
+    int rc = nkfs_fast_encode(g, ids, digests, gf, st);
+    if (rc != -ENOSYS)
+        return rc;
+    const u32 ps = max_part_size(g, g->block_size);
+    dim3 grid(g->nstripes, (ps + 255) / 256);
+    hipLaunchKernelGGL(k_encode_generic, grid, dim3(256), 0, st, *g, ids, (const GfTables *)gf);
+    if ((rc = launch_ok()))
+        return rc;
+    if (digests)
+        return nkfs_launch_hash_parts(g, digests, stream);
+    return 0;
+}
+
+extern "C" int nkfs_launch_hash_parts(const nkfs_geom *g, uint64_t *digests, void *stream)
+{
+    const u64 threads = u64(g->nstripes) * u64(g->n) * 4;
+    if (!threads)
+        return 0;
+    hipLaunchKernelGGL(k_hash_parts, dim3(u32((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *g,
+                       digests);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
+                                  int navail, void *work, int32_t *status, const void *gf, void *stream)
+{
+    if (!g->nstripes)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_decode_prep, dim3(g->nstripes), dim3(64), 0, st, ids, avail, n_slots, navail, g->k,
+                       (u8 *)work, status, (const GfTables *)gf);
+    int rc = launch_ok();
+    if (rc)
+        return rc;
+    const u32 ps = part_size_of(g->block_size, g->k);
+    dim3 grid(g->nstripes, (ps + 255) / 256);
+    hipLaunchKernelGGL(k_decode_generic, grid, dim3(256), 0, st, *g, n_slots, (const u8 *)work,
+                       (const int32_t *)status, (const GfTables *)gf);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_xxh64_stripes(uint64_t *state_v, const uint8_t *data, uint64_t nst, void *stream)
+{
+    hipLaunchKernelGGL(k_xxh64_stripes, dim3(1), dim3(64), 0, (hipStream_t)stream, state_v, data, nst);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v, uint64_t total_len,
+                                        uint64_t seed, const uint8_t *tail, uint32_t tail_len, void *stream)
+{
+    hipLaunchKernelGGL(k_xxh64_finish, dim3(1), dim3(64), 0, (hipStream_t)stream, out, state_v, total_len, seed,
+                       tail, tail_len);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                                       uint32_t count, uint64_t seed, uint64_t *out, void *stream)
+{
+    if (!count)
+        return 0;
+    const u64 threads = u64(count) * 4;
+    hipLaunchKernelGGL(k_xxh64_batch, dim3(u32((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, base,
+                       off, len, count, seed, out);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_synth(uint8_t *blocks, uint64_t pitch, uint32_t B, uint32_t nstripes, uint64_t seed,
+                                 uint64_t first, void *stream)
+{
+    if (!nstripes || !B)
+        return 0;
+    const u64 total = u64((B + 7) / 8) * nstripes;
+    const u32 grid = u32(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
+    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, (hipStream_t)stream, blocks, pitch, B, nstripes, seed,
+                       first);
+    return launch_ok();
+}

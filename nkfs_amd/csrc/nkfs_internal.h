@@ -1,0 +1,61 @@
+/* nkfs_internal.h -- contract between the C host side (nk8.c, csum.c,
+ * runtime.c) and the HIP launchers (nk8_kernels.hip).  Plain C types only. */
+#ifndef NKFS_INTERNAL_H
+#define NKFS_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Geometry of a batch of stripes in device memory.  Uniform batches set
+ * block_sizes == NULL and use (block_pitch, block_size, part_pitch); ragged
+ * batches give per-stripe block offsets/sizes and part offsets, with the
+ * part pitch of stripe s fixed at nkfs_part_pitch(block_sizes[s], k). */
+struct nkfs_geom {
+	const uint8_t *blocks;
+	uint64_t block_pitch;
+	uint32_t block_size;
+	const uint64_t *block_off;
+	const uint32_t *block_sizes;
+	uint8_t *parts;
+	uint64_t part_pitch;
+	const uint64_t *part_off;
+	uint32_t nstripes;
+	int n;
+	int k;
+};
+
+/* Launchers: return 0 or a negative errno; `stream` is a hipStream_t. */
+int nkfs_launch_gf_init(void *gf_tables, void *stream);
+int nkfs_launch_encode(const struct nkfs_geom *g, const uint8_t *ids,
+		       uint64_t *digests, const void *gf_tables, void *stream);
+int nkfs_launch_hash_parts(const struct nkfs_geom *g, uint64_t *digests,
+			   void *stream);
+int nkfs_launch_decode(const struct nkfs_geom *g, int n_slots,
+		       const uint8_t *ids, const uint8_t *avail, int navail,
+		       void *work, int32_t *status, const void *gf_tables,
+		       void *stream);
+int nkfs_launch_xxh64_stripes(uint64_t *state_v, const uint8_t *data,
+			      uint64_t nstripes32, void *stream);
+int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v,
+			     uint64_t total_len, uint64_t seed,
+			     const uint8_t *tail, uint32_t tail_len,
+			     void *stream);
+int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
+			    const uint64_t *len, uint32_t count, uint64_t seed,
+			    uint64_t *out, void *stream);
+int nkfs_launch_synth(uint8_t *blocks, uint64_t block_pitch,
+		      uint32_t block_size, uint32_t nstripes,
+		      uint64_t seed, uint64_t first_stripe, void *stream);
+
+/* Sizes shared by host and launchers. */
+uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k);
+size_t nkfs_gf_tables_bytes(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,332 @@
+/*
+ * runtime.c -- device context of libnkfs_crt.so and the batched C-ABI of
+ * include/nkfs_gpu.h.  Host C over the HIP runtime; every computation is a
+ * kernel launched through nkfs_internal.h.
+ *
+ * State: one GPU (chosen at init), one device copy of the GF(2^8)
+ * log/antilog tables, and a pool of per-call contexts (stream + growable
+ * device/pinned scratch) so that the compatibility entry points are
+ * reentrant and thread-safe after init like the reference's
+ * (SURVEY.md §8(b) "Threading").
+ */
+#include <errno.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "../../include/nkfs_gpu.h"
+#include "nkfs_internal.h"
+#include "runtime.h"
+
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static int g_ready;
+static int g_device = -1;
+static void *g_gf;
+static struct nkfs_ctx *g_pool;
+
+int nkfs_hip_fail(const char *what, int err)
+{
+	fprintf(stderr, "nkfs: %s failed: %s\n", what, hipGetErrorString((hipError_t)err));
+	return -EIO;
+}
+
+#define HIPCHK(call)                                                 \
+	do {                                                         \
+		hipError_t e_ = (call);                              \
+		if (e_ != hipSuccess)                                \
+			return nkfs_hip_fail(#call, (int)e_);        \
+	} while (0)
+
+int nkfs_gpu_init(int device)
+{
+	int rc = 0;
+	pthread_mutex_lock(&g_lock);
+	if (g_ready)
+		goto out;
+	int count = 0;
+	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+		fprintf(stderr, "nkfs: no HIP device visible; the MI355X path has no CPU fallback\n");
+		rc = -ENODEV;
+		goto out;
+	}
+	if (device < 0) {
+		const char *env = getenv("NKFS_DEVICE");
+		if (env && *env)
+			device = atoi(env);
+		else if (hipGetDevice(&device) != hipSuccess)
+			device = 0;
+	}
+	if (device >= count) {
+		rc = -ENODEV;
+		goto out;
+	}
+	hipError_t e = hipSetDevice(device);
+	if (e == hipSuccess)
+		e = hipMalloc(&g_gf, nkfs_gf_tables_bytes());
+	if (e != hipSuccess) {
+		rc = nkfs_hip_fail("device setup", (int)e);
+		goto out;
+	}
+	rc = nkfs_launch_gf_init(g_gf, NULL);
+	if (!rc && (e = hipDeviceSynchronize()) != hipSuccess)
+		rc = nkfs_hip_fail("gf table build", (int)e);
+	if (rc) {
+		hipFree(g_gf);
+		g_gf = NULL;
+		goto out;
+	}
+	g_device = device;
+	g_ready = 1;
+out:
+	pthread_mutex_unlock(&g_lock);
+	return rc;
+}
+
+int nkfs_gpu_ready(void) { return g_ready; }
+
+const void *nkfs_gf(void) { return g_gf; }
+
+static void ctx_destroy(struct nkfs_ctx *c)
+{
+	hipStreamSynchronize(c->stream);
+	hipStreamDestroy(c->stream);
+	hipFree(c->dbuf);
+	hipHostFree(c->hbuf);
+	free(c);
+}
+
+void nkfs_gpu_release(void)
+{
+	pthread_mutex_lock(&g_lock);
+	if (g_ready) {
+		hipSetDevice(g_device);
+		while (g_pool) {
+			struct nkfs_ctx *c = g_pool;
+			g_pool = c->next;
+			ctx_destroy(c);
+		}
+		hipFree(g_gf);
+		g_gf = NULL;
+		g_ready = 0;
+	}
+	pthread_mutex_unlock(&g_lock);
+}
+
+void nkfs_ctx_trim(void)
+{
+	pthread_mutex_lock(&g_lock);
+	struct nkfs_ctx *pool = g_pool;
+	g_pool = NULL;
+	pthread_mutex_unlock(&g_lock);
+	if (pool)
+		hipSetDevice(g_device);
+	while (pool) {
+		struct nkfs_ctx *c = pool;
+		pool = c->next;
+		ctx_destroy(c);
+	}
+}
+
+struct nkfs_ctx *nkfs_ctx_get(void)
+{
+	struct nkfs_ctx *c = NULL;
+	if (!g_ready)
+		return NULL;
+	pthread_mutex_lock(&g_lock);
+	if (g_pool) {
+		c = g_pool;
+		g_pool = c->next;
+	}
+	pthread_mutex_unlock(&g_lock);
+	if (hipSetDevice(g_device) != hipSuccess)
+		goto fail;
+	if (!c) {
+		c = calloc(1, sizeof(*c));
+		if (!c)
+			return NULL;
+		if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+			goto fail;
+	}
+	return c;
+fail:
+	free(c);
+	return NULL;
+}
+
+void nkfs_ctx_put(struct nkfs_ctx *c)
+{
+	if (!c)
+		return;
+	pthread_mutex_lock(&g_lock);
+	c->next = g_pool;
+	g_pool = c;
+	pthread_mutex_unlock(&g_lock);
+}
+
+int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out)
+{
+	if (bytes > c->dcap) {
+		hipStreamSynchronize(c->stream);
+		hipFree(c->dbuf);
+		c->dbuf = NULL;
+		c->dcap = 0;
+		size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+		HIPCHK(hipMalloc(&c->dbuf, cap));
+		c->dcap = cap;
+	}
+	*out = c->dbuf;
+	return 0;
+}
+
+int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out)
+{
+	if (bytes > c->hcap) {
+		hipStreamSynchronize(c->stream);
+		hipHostFree(c->hbuf);
+		c->hbuf = NULL;
+		c->hcap = 0;
+		size_t cap = bytes < (1u << 16) ? (1u << 16) : bytes;
+		HIPCHK(hipHostMalloc(&c->hbuf, cap, hipHostMallocDefault));
+		c->hcap = cap;
+	}
+	*out = c->hbuf;
+	return 0;
+}
+
+/* ------------------------------------------------------------ batch API */
+
+uint32_t nkfs_part_size(uint32_t block_size, int k)
+{
+	if (k <= 0)
+		return 0;
+	return block_size / (uint32_t)k + ((block_size % (uint32_t)k) ? 1u : 0u);
+}
+
+uint64_t nkfs_part_pitch(uint32_t block_size, int k)
+{
+	return ((uint64_t)nkfs_part_size(block_size, k) + 15) & ~(uint64_t)15;
+}
+
+/* crt/nk8.c:356-360: 2 <= k <= n <= 255, k <= 254, block_size > 0 */
+int nkfs_bad_params(uint32_t block_size, int n, int k)
+{
+	return n < 2 || k < 2 || block_size == 0 || n < k || n > 255 || k > 254;
+}
+
+int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
+		    int n, int k, const uint8_t *d_ids, uint8_t *d_parts, uint64_t part_pitch, uint64_t *d_digests,
+		    void *stream)
+{
+	if (nkfs_bad_params(block_size, n, k))
+		return -EINVAL;
+	if (!g_ready)
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!d_blocks || !d_ids || !d_parts || part_pitch < nkfs_part_size(block_size, k) || (part_pitch & 15) ||
+	    (nstripes > 1 && block_pitch < block_size))
+		return -EINVAL;
+	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
+			       nstripes, n, k };
+	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
+}
+
+int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off, const uint32_t *d_block_size,
+			   uint32_t max_block_size, uint32_t nstripes, int n, int k, const uint8_t *d_ids,
+			   uint8_t *d_parts, const uint64_t *d_part_off, uint64_t *d_digests, void *stream)
+{
+	if (nkfs_bad_params(max_block_size, n, k))
+		return -EINVAL;
+	if (!g_ready)
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!d_blocks || !d_block_off || !d_block_size || !d_ids || !d_parts || !d_part_off)
+		return -EINVAL;
+	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
+			       nstripes, n, k };
+	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
+}
+
+uint64_t nkfs_decode_workspace(uint32_t nstripes, int k)
+{
+	return nkfs_decode_work_bytes(nstripes, k);
+}
+
+int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
+		    const uint8_t *d_avail, int navail, int k, uint32_t block_size, uint8_t *d_blocks,
+		    uint64_t block_pitch, uint32_t nstripes, void *d_work, int32_t *d_status, void *stream)
+{
+	if (nkfs_bad_params(block_size, navail, k) || n_slots < 1 || n_slots > 255)
+		return -EINVAL;
+	if (!g_ready)
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!d_parts || !d_ids || !d_avail || !d_blocks || !d_work || part_pitch < nkfs_part_size(block_size, k) ||
+	    (nstripes > 1 && block_pitch < block_size))
+		return -EINVAL;
+	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
+			       nstripes, n_slots, k };
+	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream);
+}
+
+int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off, const uint64_t *d_len, uint32_t count,
+		     uint64_t seed, uint64_t *d_out, void *stream)
+{
+	if (!g_ready)
+		return -EAGAIN;
+	if (count && (!d_base || !d_off || !d_len || !d_out))
+		return -EINVAL;
+	return nkfs_launch_xxh64_batch(d_base, d_off, d_len, count, seed, d_out, stream);
+}
+
+int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
+		      uint64_t seed, uint64_t first_stripe, void *stream)
+{
+	if (!g_ready)
+		return -EAGAIN;
+	if (nstripes && (!d_blocks || (nstripes > 1 && block_pitch < block_size)))
+		return -EINVAL;
+	return nkfs_launch_synth(d_blocks, block_pitch, block_size, nstripes, seed, first_stripe, stream);
+}
+
+void *nkfs_dev_alloc(size_t bytes)
+{
+	void *p = NULL;
+	if (!g_ready || hipSetDevice(g_device) != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess)
+		return NULL;
+	return p;
+}
+
+void nkfs_dev_free(void *p)
+{
+	if (p)
+		hipFree(p);
+}
+
+int nkfs_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+	HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+	return 0;
+}
+
+int nkfs_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+	HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int nkfs_stream_sync(void *stream)
+{
+	HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+	return 0;
+}
+
+/* ------------------------------------------------------------- memory */
+
+void *crt_malloc(size_t size) { return malloc(size); }
+void crt_free(void *ptr) { free(ptr); }

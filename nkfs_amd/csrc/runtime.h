@@ -1,0 +1,29 @@
+/* runtime.h -- host-side context shared by runtime.c, nk8.c and csum.c. */
+#ifndef NKFS_RUNTIME_H
+#define NKFS_RUNTIME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+struct nkfs_ctx {
+	hipStream_t stream;
+	void *dbuf;   /* device scratch */
+	size_t dcap;
+	void *hbuf;   /* pinned host scratch */
+	size_t hcap;
+	struct nkfs_ctx *next;
+};
+
+struct nkfs_ctx *nkfs_ctx_get(void);
+void nkfs_ctx_put(struct nkfs_ctx *c);
+int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out);
+int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out);
+const void *nkfs_gf(void);
+void nkfs_gpu_release(void);
+void nkfs_ctx_trim(void);
+int nkfs_bad_params(uint32_t block_size, int n, int k);
+int nkfs_hip_fail(const char *what, int err);
+
+#endif

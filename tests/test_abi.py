@@ -1,0 +1,83 @@
+"""The drop-in boundary: libnkfs_crt.so loads, exports every function
+include/*.h declares, validates arguments like the reference, and refuses to
+compute without a GPU (no CPU fallback).  No compute calls happen here."""
+import ctypes as C
+import subprocess
+
+import pytest
+
+from conftest import has_gpu_device
+from nkfs_amd import _lib
+
+REFERENCE_SYMBOLS = [  # crt/include/nk8.h:4-11, csum.h:14-17, xxhash.h:86-132, crt.h:12-13
+    "nk8_init", "nk8_release", "nk8_split_block", "nk8_assemble_block",
+    "csum_reset", "csum_update", "csum_digest", "csum_u64",
+    "XXH64", "XXH64_createState", "XXH64_freeState", "XXH64_reset", "XXH64_update", "XXH64_digest",
+    "crt_malloc", "crt_free",
+]
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    return {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+
+
+def test_library_loads():
+    assert _lib.lib() is not None
+
+
+def test_every_header_function_is_exported():
+    names = _lib.header_functions()
+    assert len(names) >= 30
+    syms = exported()
+    missing = [n for n in names if n not in syms]
+    assert not missing, missing
+    # and nothing beyond the declared ABI leaks out
+    assert syms <= set(names)
+
+
+def test_reference_symbols_present():
+    syms = exported()
+    for s in REFERENCE_SYMBOLS:
+        assert s in syms
+
+
+def test_state_abi_size():
+    # struct csum_ctx embeds XXH64_state_t by value: 11 long longs (xxhash.h:105)
+    assert C.sizeof(C.c_longlong * 11) == 88
+
+
+def test_argument_validation_matches_reference():
+    L = _lib.lib()
+    u8p = _lib.u8p
+    buf = (C.c_uint8 * 16)()
+    pp = C.POINTER(u8p)()
+    pi = u8p()
+    # crt/nk8.c:356-360 -- checked before the init check
+    for B, n, k in [(0, 4, 2), (16, 4, 1), (16, 2, 3), (16, 256, 2), (16, 255, 255)]:
+        assert L.nk8_split_block(buf, B, n, k, C.byref(pp), C.byref(pi)) == -22
+    parts = (u8p * 4)()
+    ids = (C.c_uint8 * 4)(1, 2, 3, 4)
+    assert L.nk8_assemble_block(parts, ids, 1, 2, buf, 16) == -22
+
+
+@pytest.mark.skipif(has_gpu_device(), reason="checks the no-GPU behaviour")
+def test_no_gpu_fails_loudly():
+    L = _lib.lib()
+    assert L.nk8_init() == -19  # -ENODEV
+    assert L.nkfs_gpu_ready() == 0
+    u8p = _lib.u8p
+    buf = (C.c_uint8 * 4096)()
+    pp = C.POINTER(u8p)()
+    pi = u8p()
+    assert L.nk8_split_block(buf, 4096, 4, 2, C.byref(pp), C.byref(pi)) == -11  # -EAGAIN
+    assert L.nkfs_nk8_encode(None, 4096, 4096, 1, 4, 2, None, None, 2048, None, None) == -11
+    assert L.nkfs_dev_alloc(16) is None
+
+
+def test_part_geometry():
+    L = _lib.lib()
+    assert L.nkfs_part_size(1048576, 5) == 209716
+    assert L.nkfs_part_pitch(1048576, 5) == 209728
+    assert L.nkfs_part_size(4096, 2) == 2048
+    assert L.nkfs_part_pitch(1, 2) == 16

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP path through the C-ABI against the reference's golden
+vectors and the pinned CPU oracle, bit-exact (integer/byte arithmetic).
+
+Sizes: golden cases in full; BASELINE configs at full per-stripe size with
+stripe counts the oracle checks in seconds; C2 (65,536 x 4 KiB) in full.
+Full-size properties: encode -> erase -> decode round trips on the device.
+"""
+import ctypes as C
+import hashlib
+
+import numpy as np
+import pytest
+
+from nkfs_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nkfs_amd import _lib
+    lib = _lib.lib()
+    assert lib.nk8_init() == 0, "nk8_init (GPU self test) failed"
+    assert lib.nkfs_gpu_ready() == 1
+    return lib
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def u64(x):
+    return int(x) & 0xFFFFFFFFFFFFFFFF
+
+
+def encode_batch(blocks_np, n, k, ids_np, block_size):
+    from nkfs_amd import batch
+    blocks = dev(blocks_np)
+    ids = dev(ids_np)
+    parts, dig = batch.encode(blocks, block_size, n, k, ids)
+    torch.cuda.synchronize()
+    return blocks, parts, dig
+
+
+# ------------------------------------------------------------------ golden
+
+def test_encode_golden(L, golden):
+    from nkfs_amd import batch
+    for case in golden["encode"]:
+        B, n, k = case["block_size"], case["n"], case["k"]
+        blk = synth.stripe_bytes(case["stripe"], B)
+        ids = np.frombuffer(bytes.fromhex(case["ids"]), dtype=np.uint8)[None, :]
+        pitch = ((B + 15) // 16) * 16
+        host = np.zeros((1, pitch), np.uint8)
+        host[0, :B] = blk
+        _, parts, dig = encode_batch(host, n, k, ids, B)
+        ps = batch.part_size(B, k)
+        got = parts[:, :ps].cpu().numpy()
+        assert sha(got) == case["parts_sha256"], (B, n, k)
+        assert [f"{u64(d):016x}" for d in dig.cpu().tolist()] == case["part_xxh64"], (B, n, k)
+
+
+def test_decode_golden(L, golden, O):
+    from nkfs_amd import batch
+    enc = golden["encode"]
+    for d in golden["decode"]:
+        case = enc[d["case"]]
+        B, n, k = case["block_size"], case["n"], case["k"]
+        blk = synth.stripe_bytes(case["stripe"], B)
+        ids = np.frombuffer(bytes.fromhex(case["ids"]), dtype=np.uint8)
+        parts = O.encode(blk, n, k, ids)
+        pitch = batch.part_pitch(B, k)
+        slots = np.zeros((n, pitch), np.uint8)
+        slots[:, : parts.shape[1]] = parts
+        avail = np.array(d["order"], dtype=np.uint8)[None, :]
+        navail = avail.shape[1]
+        if navail < 2 or navail < k:
+            # fewer offered parts than k: the API rejects like nk8_assemble_block
+            assert d["err"] == -22
+            continue
+        out, status = batch.decode(dev(slots), n, dev(ids[None, :]), dev(avail), k, B)
+        torch.cuda.synchronize()
+        assert int(status[0]) == d["err"], (B, n, k, d["order"])
+        if d["err"] == 0:
+            assert sha(out[0].cpu().numpy()) == d["block_sha256"]
+
+
+def test_xxh64_golden_batch_and_compat(L, golden):
+    from nkfs_amd import batch, crt
+    vecs = golden["xxh64"]
+    datas = [synth.stripe_bytes(v["stripe"], v["len"]) if v["len"] else np.zeros(0, np.uint8) for v in vecs]
+    # batch API, per seed
+    for seed_hex in sorted({v["seed"] for v in vecs}):
+        sel = [i for i, v in enumerate(vecs) if v["seed"] == seed_hex]
+        offs, buf, pos = [], [], 0
+        for i in sel:
+            offs.append(pos)
+            buf.append(datas[i])
+            pad = (-len(datas[i])) % 8 + 8
+            buf.append(np.zeros(pad, np.uint8))
+            pos += len(datas[i]) + pad
+        base = dev(np.concatenate(buf))
+        off = dev(np.array(offs, np.uint64).view(np.int64))
+        lens = dev(np.array([len(datas[i]) for i in sel], np.uint64).view(np.int64))
+        got = batch.xxh64_batch(base, off, lens, seed=int(seed_hex, 16))
+        want = [int(vecs[i]["digest"], 16) for i in sel]
+        assert [u64(x) for x in got.cpu().tolist()] == want
+    # drop-in one-shot XXH64 (seed 0 subset)
+    for v, data in zip(vecs, datas):
+        assert crt.xxh64(data, int(v["seed"], 16)) == int(v["digest"], 16)
+
+
+def test_csum_streaming_matches_oracle(L, O):
+    from nkfs_amd import crt
+    rng = np.random.default_rng(3)
+    for total in [0, 1, 31, 32, 33, 100, 4096, 65536 + 13]:
+        data = rng.integers(0, 256, total, dtype=np.uint8)
+        cs = crt.Csum()
+        pos = 0
+        while pos < total:
+            step = int(rng.integers(1, 97))
+            cs.update(data[pos: pos + step])
+            pos += step
+        assert cs.digest() == O.xxh64(data)
+
+
+# -------------------------------------------------------------- drop-in API
+
+def test_split_assemble_compat(L, O):
+    from nkfs_amd import crt
+    rng = np.random.default_rng(5)
+    for B, n, k in [(4096, 4, 2), (1048576, 8, 5), (70000, 255, 254), (1, 2, 2), (13, 8, 5), (65537, 16, 9)]:
+        blk = rng.integers(0, 256, B, dtype=np.uint8)
+        parts, ids = crt.split_block(blk, n, k)
+        assert len(set(ids.tolist())) == n and ids.min() >= 1
+        want = O.encode(blk, n, k, ids)
+        assert np.array_equal(np.stack(parts), want)
+        sel = rng.permutation(n)[:k]
+        out = crt.assemble_block([parts[i] for i in sel], ids[sel], k, k, B)
+        assert np.array_equal(out, blk)
+        # extra parts after the first k distinct are ignored, duplicates skipped
+        order = [int(sel[0])] + [int(x) for x in rng.permutation(n)]
+        out2 = crt.assemble_block([parts[i] for i in order], ids[order], len(order), k, B)
+        assert np.array_equal(out2, blk)
+
+
+def test_compat_errors(L, golden):
+    from nkfs_amd import crt
+    for e in golden["split_errors"]:
+        blk = np.zeros(max(e["block_size"], 1), np.uint8)[: e["block_size"]]
+        with pytest.raises(OSError) as ei:
+            crt.split_block(blk, e["n"], e["k"])
+        assert -ei.value.errno == e["err"]
+    parts, ids = crt.split_block(np.arange(100, dtype=np.uint8), 4, 3)
+    with pytest.raises(OSError) as ei:  # two distinct ids offered, k = 3
+        crt.assemble_block([parts[0], parts[0], parts[1], parts[1]], [ids[0], ids[0], ids[1], ids[1]], 4, 3, 100)
+    assert ei.value.errno == 22
+
+
+def test_synth_kernel_matches_numpy(L):
+    from nkfs_amd import batch
+    for B in (4096, 1000, 13):
+        t = batch.synth(9, B, first=40)
+        torch.cuda.synchronize()
+        got = t[:, :B].cpu().numpy()
+        assert np.array_equal(got, synth.batch_bytes(9, B, first=40))
+
+
+# --------------------------------------------------------- BASELINE shapes
+
+def _oracle_digests(O, blocks_np, ids_np, n, k, B):
+    out = []
+    for s in range(blocks_np.shape[0]):
+        parts = O.encode(blocks_np[s, :B], n, k, ids_np[s])
+        out.extend(O.xxh64(p) for p in parts)
+    return out
+
+
+def test_c2_full_batch_n4k2_4k(L, O):
+    """configs[1]: N=4,K=2 encode of 64 Ki x 4 KiB stripes, every part's bytes
+    checked through its XXH64 against the oracle, then erase 2 -> decode."""
+    from nkfs_amd import batch
+    S, B, n, k = 65536, 4096, 4, 2
+    blocks = batch.synth(S, B)
+    ids_np = synth.batch_ids(S, n)
+    parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    blocks_np = blocks.cpu().numpy()
+    want = _oracle_digests(O, blocks_np, ids_np, n, k, B)
+    got = [u64(x) for x in dig.cpu().tolist()]
+    assert got == want
+    # spot-check raw part bytes too
+    for s in (0, 1, 12345, S - 1):
+        assert np.array_equal(parts[s * n:(s + 1) * n, :2048].cpu().numpy(),
+                              O.encode(blocks_np[s, :B], n, k, ids_np[s]))
+    avail = dev(synth.batch_survivors(S, n, k))
+    out, status = batch.decode(parts, n, dev(ids_np), avail, k, B)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])
+
+
+@pytest.mark.parametrize("S,B,n,k,keep", [
+    (48, 1048576, 8, 5, 5),    # C3 shape: 1 MiB stripes, decode from 5 of 8
+    (256, 262144, 8, 5, 5),    # C4: 256 KiB, 3 erased
+    (512, 65536, 8, 5, 6),     # extra survivor offered
+    (64, 70000, 255, 254, 254),
+    (300, 777, 17, 16, 17),
+])
+def test_uniform_shapes(L, O, S, B, n, k, keep):
+    from nkfs_amd import batch
+    blocks = batch.synth(S, B, first=7)
+    ids_np = synth.batch_ids(S, n, first=7)
+    parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    blocks_np = blocks.cpu().numpy()
+    check = list(range(0, S, max(1, S // 16)))
+    for s in check:
+        want = _oracle_digests(O, blocks_np[s:s + 1], ids_np[s:s + 1], n, k, B)
+        got = [u64(x) for x in dig[s * n:(s + 1) * n].cpu().tolist()]
+        assert got == want, s
+    avail = dev(synth.batch_survivors(S, n, keep, first=7))
+    out, status = batch.decode(parts, n, dev(ids_np), avail, k, B)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])
+
+
+def test_ragged_mixed_batch(L, O):
+    """C5 shape: mixed 4 KiB / 64 KiB / 1 MiB stripes in one ragged batch,
+    N=8,K=5 and the N=4,K=2 variant, digests against the oracle."""
+    from nkfs_amd import batch
+    for n, k in ((8, 5), (4, 2)):
+        sizes = synth.mixed_sizes(40)
+        sizes[:3] = (4096, 65536, 1048576)
+        boff = np.zeros(len(sizes), np.int64)
+        poff = np.zeros(len(sizes), np.int64)
+        pos = ppos = 0
+        for s, B in enumerate(sizes):
+            boff[s] = pos
+            poff[s] = ppos
+            pos += ((int(B) + 15) // 16) * 16
+            ppos += n * batch.part_pitch(int(B), k)
+        host = np.zeros(pos, np.uint8)
+        for s, B in enumerate(sizes):
+            host[boff[s]: boff[s] + B] = synth.stripe_bytes(s, int(B))
+        ids_np = synth.batch_ids(len(sizes), n)
+        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+        batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts,
+                            dev(poff), dig, int(sizes.max()))
+        torch.cuda.synchronize()
+        got = [u64(x) for x in dig.cpu().tolist()]
+        for s, B in enumerate(sizes):
+            want = _oracle_digests(O, host[None, boff[s]: boff[s] + B], ids_np[s:s + 1], n, k, int(B))
+            assert got[s * n:(s + 1) * n] == want, (s, B)
+
+
+def test_decode_status_too_few_distinct(L):
+    from nkfs_amd import batch
+    S, B, n, k = 4, 4096, 4, 2
+    blocks = batch.synth(S, B)
+    ids_np = synth.batch_ids(S, n)
+    parts, _ = batch.encode(blocks, B, n, k, dev(ids_np), digests=False)
+    ids_dup = ids_np.copy()
+    ids_dup[1, 1] = ids_dup[1, 0]  # stripe 1: slots 0 and 1 share an id
+    avail = np.tile(np.array([0, 1], np.uint8), (S, 1))
+    out, status = batch.decode(parts, n, dev(ids_dup), dev(avail), k, B)
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    assert st[1] == -22 and st[0] == st[2] == st[3] == 0
+    assert torch.equal(out[0], blocks[0, :B]) and torch.equal(out[3], blocks[3, :B])
