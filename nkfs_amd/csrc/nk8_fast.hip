@@ -1,9 +1,333 @@
-// nk8_fast.hip -- streaming fast path (placeholder until the fused kernel lands)
+// nk8_fast.hip -- streaming fast path of the nkfs N-K encode for n <= 8:
+// encode fused with XXH64 of every part, one pass over HBM.
+//
+// Reference: crt/nk8.c:403-420 (part_i[j] = XOR_m ids[i]^m * d[j*k+m]) and
+// crt/xxhash.c:358-496 (XXH64, seed 0 as crt/csum.c:5), per part.
+//
+// Shape of one workgroup = one wave (64 lanes) = G stripes in lock step:
+//   E = 4 (n <= 4): G = 4 stripes, 16 lanes per stripe, chunk R = 256 rows
+//   E = 8 (n <= 8): G = 2 stripes, 32 lanes per stripe, chunk R = 512 rows
+// so that 4 lanes x n parts x G stripes <= 64 hash chains fill the wave: XXH64
+// of one part is serial, its only parallelism being its four accumulators,
+// so every lane owns one (stripe, part, accumulator) chain for the whole
+// stripe and the chunk loop feeds it 8-byte words in order.
+//
+// Per chunk each lane encodes 16 consecutive rows of its stripe (16*k input
+// bytes: k x 16-byte loads, coalesced across lanes):
+//   row r -> E packed bytes  = rep(d[r*k]) ^ XOR_{m>=1} T_m[d[r*k+m]]
+// where T_m[x] = (ids[0]^m * x, ..., ids[n-1]^m * x) is a per-stripe packed
+// product table in LDS (built from eight basis products: multiplication by a
+// constant is GF(2)-linear), so one LDS lookup yields the term for all n parts
+// and column m = 0 (coefficient 1) needs no lookup at all.  A byte transpose
+// (v_perm) turns 16 rows x E bytes into 16 bytes per part, which go to HBM
+// (one 16-byte store per part) and to an LDS exchange buffer from which the
+// hash lanes take their words.
 #include <hip/hip_runtime.h>
 #include <errno.h>
-#include "nkfs_internal.h"
+#include <stdint.h>
 
-extern "C" int nkfs_fast_encode(const nkfs_geom *, const uint8_t *, uint64_t *, const void *, hipStream_t)
+#include "gf256.h"
+#include "nkfs_internal.h"
+#include "xxh64_dev.h"
+
+using namespace nkfs;
+typedef uint8_t u8;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+namespace {
+
+__device__ inline u32 part_size_of(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
+
+// per-byte GF product of two packed words (a_i * b_i for each byte i)
+__device__ inline u32 gf_mul_packed(u32 a, u32 b)
 {
-    return -ENOSYS;
+    u32 r = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        const u32 mask = ((b >> bit) & 0x01010101u) * 0xFFu;
+        r ^= a & mask;
+        a = gf_xtime4(a);
+    }
+    return r;
+}
+
+// 4x4 byte transpose: in[r] byte c -> out[c] byte r
+__device__ inline void transpose4(u32 a, u32 b, u32 c, u32 d, u32 &o0, u32 &o1, u32 &o2, u32 &o3)
+{
+    // v_perm_b32(S0, S1, sel): selector 0-3 -> S1 bytes, 4-7 -> S0 bytes
+    const u32 t0 = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
+    const u32 t1 = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
+    const u32 t2 = __builtin_amdgcn_perm(d, c, 0x05010400u);  // c0 d0 c1 d1
+    const u32 t3 = __builtin_amdgcn_perm(d, c, 0x07030602u);  // c2 d2 c3 d3
+    o0 = __builtin_amdgcn_perm(t2, t0, 0x05040100u);         // a0 b0 c0 d0
+    o1 = __builtin_amdgcn_perm(t2, t0, 0x07060302u);         // a1 b1 c1 d1
+    o2 = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+    o3 = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+__device__ inline u64 shfl64(u64 v, int src)
+{
+    u32 lo = __shfl(u32(v), src, 64);
+    u32 hi = __shfl(u32(v >> 32), src, 64);
+    return (u64(hi) << 32) | lo;
+}
+
+struct Stripe {
+    const u8 *blk;
+    u8 *parts;
+    u64 pitch;
+    u32 B;
+    u32 ps;
+};
+
+__device__ inline Stripe stripe_at(const nkfs_geom &g, u32 s)
+{
+    Stripe v;
+    if (g.block_sizes) {
+        v.B = g.block_sizes[s];
+        v.blk = g.blocks + g.block_off[s];
+        v.parts = g.parts + g.part_off[s];
+        v.ps = part_size_of(v.B, g.k);
+        v.pitch = (u64(v.ps) + 15) & ~u64(15);
+    } else {
+        v.B = g.block_size;
+        v.blk = g.blocks + u64(s) * g.block_pitch;
+        v.parts = g.parts + u64(s) * u64(g.n) * g.part_pitch;
+        v.ps = part_size_of(v.B, g.k);
+        v.pitch = g.part_pitch;
+    }
+    return v;
+}
+
+}  // namespace
+
+template <int K, int E, bool HASH>
+__global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, u64 *digests)
+{
+    constexpr int G = E == 4 ? 4 : 2;   // stripes per wave
+    constexpr int LP = 64 / G;          // lanes per stripe
+    constexpr int R = 16 * LP;          // rows per stripe per chunk
+    constexpr int SP = R + 32;          // LDS bytes per part in the exchange buffer (bank spread)
+    constexpr int TB = 256 * E;         // bytes per packed table
+    constexpr int W = E / 4;            // dwords per packed entry
+    __shared__ __attribute__((aligned(16))) u8 tbl[G * (K - 1) * TB];
+    __shared__ __attribute__((aligned(16))) u8 xbuf[G * E * SP];
+
+    const int lane = threadIdx.x;
+    const int gi = lane / LP;
+    const int li = lane % LP;
+    const int n = g.n;
+    const u32 s = blockIdx.x * G + gi;
+    const bool live = s < g.nstripes;
+    Stripe v{};
+    if (live)
+        v = stripe_at(g, s);
+
+    // ---- packed product tables T_m, m = 1..K-1, for this lane's stripe
+    u32 coef[W];  // packed ids[i]^m
+    u32 idw[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        u32 x = 0;
+        if (live)
+            for (int b = 0; b < 4; ++b)
+                if (4 * w + b < n)
+                    x |= u32(ids[u64(s) * n + 4 * w + b]) << (8 * b);
+        idw[w] = x;
+        coef[w] = x;
+    }
+    u8 *mytbl = tbl + gi * (K - 1) * TB;
+#pragma unroll
+    for (int m = 1; m < K; ++m) {
+        u32 basis[8][W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            u32 x = coef[w];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                basis[b][w] = x;
+                x = gf_xtime4(x);
+            }
+        }
+        for (int x = li; x < 256; x += LP) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                u32 e = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
+                *reinterpret_cast<u32 *>(mytbl + (m - 1) * TB + x * E + 4 * w) = e;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            coef[w] = gf_mul_packed(coef[w], idw[w]);
+    }
+    __syncthreads();
+
+    // ---- hash chain of this lane: part hi, accumulator ha
+    const int hi = li >> 2, ha = li & 3;
+    const bool hlane = HASH && live && hi < n;
+    u64 acc = xxh_acc_init(ha, 0);
+    const u32 nst = v.ps >> 5;  // whole 32-byte stripes of each part
+    const u32 nchunks = live ? (v.ps + R - 1) / R : 0;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
+
+    for (u32 c = 0; __any(c < nchunks); ++c) {
+        const u32 r0 = c * R + 16 * li;
+        if (c < nchunks && r0 < v.ps) {
+            // 16 rows = 16*K input bytes
+            u32 d[4 * K];
+            const u64 off = u64(r0) * K;
+            if (aligned && off + 16 * K <= v.B) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const uint4 t = src[q];
+                    d[4 * q] = t.x;
+                    d[4 * q + 1] = t.y;
+                    d[4 * q + 2] = t.z;
+                    d[4 * q + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4 * K; ++q) {
+                    u32 x = 0;
+                    for (int b = 0; b < 4; ++b) {
+                        const u64 p = off + 4 * q + b;
+                        if (p < v.B)
+                            x |= u32(v.blk[p]) << (8 * b);
+                    }
+                    d[q] = x;
+                }
+            }
+            u32 row[16][W];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                constexpr int dummy = 0;
+                (void)dummy;
+                const int p0 = r * K;
+                const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    row[r][w] = rep;
+#pragma unroll
+                for (int m = 1; m < K; ++m) {
+                    const int p = p0 + m;
+                    const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                    const u8 *e = mytbl + (m - 1) * TB + byte * E;
+                    if constexpr (E == 8) {
+                        const uint2 t = *reinterpret_cast<const uint2 *>(e);
+                        row[r][0] ^= t.x;
+                        row[r][1] ^= t.y;
+                    } else {
+                        row[r][0] ^= *reinterpret_cast<const u32 *>(e);
+                    }
+                }
+            }
+            // rows -> parts: out[i][q] = bytes of part i for rows 4q..4q+3
+            u32 out[E][4];
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    transpose4(row[4 * q][w], row[4 * q + 1][w], row[4 * q + 2][w], row[4 * q + 3][w],
+                               out[4 * w][q], out[4 * w + 1][q], out[4 * w + 2][q], out[4 * w + 3][q]);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                if (i < n) {
+                    const uint4 val = make_uint4(out[i][0], out[i][1], out[i][2], out[i][3]);
+                    u8 *dst = v.parts + u64(i) * v.pitch + r0;
+                    if (aligned) {
+                        *reinterpret_cast<uint4 *>(dst) = val;
+                    } else {
+                        for (int b = 0; b < 16 && r0 + b < v.ps; ++b)
+                            dst[b] = u8(out[i][b >> 2] >> (8 * (b & 3)));
+                    }
+                    if constexpr (HASH)
+                        *reinterpret_cast<uint4 *>(xbuf + (gi * E + i) * SP + 16 * li) = val;
+                }
+            }
+        }
+        if constexpr (HASH) {
+            __syncthreads();
+            if (hlane && c < nchunks) {
+                const u8 *src = xbuf + (gi * E + hi) * SP + 8 * ha;
+                const u32 first = c * (R / 32);
+#pragma unroll 4
+                for (int rr = 0; rr < R / 32; ++rr) {
+                    if (first + rr < nst)
+                        acc = xxh_round(acc, *reinterpret_cast<const u64 *>(src + 32 * rr));
+                }
+            }
+            __syncthreads();
+        }
+    }
+
+    if constexpr (HASH) {
+        const int base = lane & ~3;
+        const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+        const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+        if (hlane && ha == 0) {
+            u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+            h += v.ps;
+            u64 tw[4] = {0, 0, 0, 0};
+            const u32 left = v.ps & 31;
+            if (left) {
+                // the tail sits in the last chunk's exchange buffer
+                const u32 toff = nst * 32 - (nchunks - 1) * R;
+                const u64 *src = reinterpret_cast<const u64 *>(xbuf + (gi * E + hi) * SP + toff);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    tw[w] = src[w];
+            }
+            digests[u64(s) * n + hi] = xxh_tail_regs(h, tw, left);
+        }
+    }
+}
+
+template <int E, bool HASH>
+static int launch_k(int k, dim3 grid, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig)
+{
+    switch (k) {
+#define NKFS_K(KK)                                                                        \
+    case KK:                                                                              \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, HASH>), grid, dim3(64), 0, st, g, ids, dig); \
+        return 0;
+        NKFS_K(2)
+        NKFS_K(3)
+        NKFS_K(4)
+        NKFS_K(5)
+        NKFS_K(6)
+        NKFS_K(7)
+        NKFS_K(8)
+#undef NKFS_K
+    default:
+        return -ENOSYS;
+    }
+}
+
+// Returns -ENOSYS when the shape is outside the fast path (the caller then
+// uses the generic kernels).
+extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *,
+                                hipStream_t st)
+{
+    if (getenv("NKFS_FORCE_GENERIC"))
+        return -ENOSYS;
+    if (g->n > 8 || g->k > 8)
+        return -ENOSYS;
+    const int E = g->n <= 4 ? 4 : 8;
+    const int G = E == 4 ? 4 : 2;
+    const dim3 grid((g->nstripes + G - 1) / G);
+    int rc;
+    if (E == 4)
+        rc = digests ? launch_k<4, true>(g->k, grid, st, *g, ids, digests)
+                     : launch_k<4, false>(g->k, grid, st, *g, ids, digests);
+    else
+        rc = digests ? launch_k<8, true>(g->k, grid, st, *g, ids, digests)
+                     : launch_k<8, false>(g->k, grid, st, *g, ids, digests);
+    if (rc)
+        return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

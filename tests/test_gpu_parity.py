@@ -151,7 +151,7 @@ def test_split_assemble_compat(L, O):
         out = crt.assemble_block([parts[i] for i in sel], ids[sel], k, k, B)
         assert np.array_equal(out, blk)
         # extra parts after the first k distinct are ignored, duplicates skipped
-        order = [int(sel[0])] + [int(x) for x in rng.permutation(n)]
+        order = [int(sel[0])] + [int(x) for x in rng.permutation(n)][: min(n, 254)]
         out2 = crt.assemble_block([parts[i] for i in order], ids[order], len(order), k, B)
         assert np.array_equal(out2, blk)
 
