@@ -331,3 +331,221 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+
+// ------------------------------------------------------------------ decode
+//
+// One wave per stripe, k <= 8 (crt/nk8.c:446-599):
+//  1. lane 0 picks the first k offered parts with distinct ids
+//     (crt/nk8.c:512-537) and forms M(t) = prod_c (t + x_c);
+//  2. lane c < k computes row c of W = V^-1 for V[m][c] = x_c^m in closed
+//     form (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) / M'(x_c)), which
+//     is the unique inverse the reference's Gauss-Jordan produces;
+//  3. packed tables U_c[x] = (W[c][0]*x, ..., W[c][k-1]*x) go to LDS;
+//  4. every lane rebuilds 16 rows per step: one 16-byte load from each of the
+//     k parts, k*16 lookups, rows packed back to k*16 contiguous bytes:
+//       block[j*k + m] = XOR_c part_c[j] * W[c][m]      (crt/nk8.c:552-582)
+namespace {
+
+struct GfL {
+    uint16_t log[256];
+    u8 exp[768];
+};
+
+__device__ inline u8 lmul(const GfL &L, u8 a, u8 b) { return (a && b) ? L.exp[L.log[a] + L.log[b]] : u8(0); }
+__device__ inline u8 ldiv(const GfL &L, u8 a, u8 b) { return (a && b) ? L.exp[L.log[a] + 255 - L.log[b]] : u8(0); }
+
+}  // namespace
+
+template <int K, int E>
+__global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
+                                                    int navail, int32_t *status, const GfTables *gft)
+{
+    constexpr int W = E / 4;
+    constexpr int TB = 256 * E;
+    constexpr int R = 16 * 64;  // rows per step
+    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
+    __shared__ GfL L;
+    __shared__ u8 xs[K], slot[K], M[K + 1], wrow[K][K];
+    __shared__ int have;
+
+    const int lane = threadIdx.x;
+    const u32 s = blockIdx.x;
+    for (int i = lane; i < 256; i += 64)
+        L.log[i] = gft->log[i];
+    for (int i = lane; i < 768; i += 64)
+        L.exp[i] = gft->exp[i];
+    __syncthreads();
+    if (lane == 0) {
+        const u8 *sid = ids + u64(s) * n_slots;
+        const u8 *sav = avail + u64(s) * navail;
+        int h = 0;
+        for (int c = 0; c < navail && h < K; ++c) {
+            const u8 id = sid[sav[c]];
+            bool dup = false;
+            for (int d = 0; d < c; ++d)
+                dup |= sid[sav[d]] == id;
+            if (dup)
+                continue;
+            xs[h] = id;
+            slot[h] = sav[c];
+            ++h;
+        }
+        have = h;
+        if (status)
+            status[s] = h < K ? -EINVAL : 0;
+        if (h == K) {
+            M[0] = 1;
+            for (int c = 0; c < K; ++c) {
+                M[c + 1] = M[c];
+                for (int i = c; i >= 1; --i)
+                    M[i] = M[i - 1] ^ lmul(L, xs[c], M[i]);
+                M[0] = lmul(L, xs[c], M[0]);
+            }
+        }
+    }
+    __syncthreads();
+    if (have < K)
+        return;
+    if (lane < K) {
+        const u8 xc = xs[lane];
+        u8 q[K];
+        u8 acc = M[K];
+        q[K - 1] = acc;
+#pragma unroll
+        for (int i = K - 1; i >= 1; --i) {
+            acc = M[i] ^ lmul(L, xc, acc);
+            q[i - 1] = acc;
+        }
+        u8 d = 0;
+#pragma unroll
+        for (int i = K - 1; i >= 0; --i)
+            d = lmul(L, d, xc) ^ q[i];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            wrow[lane][i] = ldiv(L, q[i], d);
+    }
+    __syncthreads();
+    // packed tables U_c, entries x = lane, lane+64, ...
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        u32 basis[8][W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            u32 x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (4 * w + b < K)
+                    x |= u32(wrow[c][4 * w + b]) << (8 * b);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                basis[b][w] = x;
+                x = gf_xtime4(x);
+            }
+        }
+        for (int x = lane; x < 256; x += 64) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                u32 e = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b)
+                    e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
+                *reinterpret_cast<u32 *>(tbl + c * TB + x * E + 4 * w) = e;
+            }
+        }
+    }
+    __syncthreads();
+
+    const u32 B = g.block_size;
+    const u32 ps = part_size_of(B, K);
+    const u8 *src[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+        src[c] = g.parts + (u64(s) * n_slots + slot[c]) * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
+
+    for (u32 r0 = 16 * lane; r0 < ps; r0 += R) {
+        u32 pv[K][4];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
+            pv[c][0] = t.x;
+            pv[c][1] = t.y;
+            pv[c][2] = t.z;
+            pv[c][3] = t.w;
+        }
+        u32 row[16][W];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                row[r][w] = 0;
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                const u8 *e = tbl + c * TB + byte * E;
+                if constexpr (E == 8) {
+                    const uint2 t = *reinterpret_cast<const uint2 *>(e);
+                    row[r][0] ^= t.x;
+                    row[r][1] ^= t.y;
+                } else {
+                    row[r][0] ^= *reinterpret_cast<const u32 *>(e);
+                }
+            }
+        }
+        // pack 16 rows of K bytes into 4*K dwords (byte p = r*K + m)
+        u32 o[4 * K];
+#pragma unroll
+        for (int q = 0; q < 4 * K; ++q) {
+            u32 x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int p = 4 * q + b;
+                const int r = p / K, m = p % K;
+                x |= ((row[r][m >> 2] >> (8 * (m & 3))) & 0xFFu) << (8 * b);
+            }
+            o[q] = x;
+        }
+        const u64 off = u64(r0) * K;
+        if (aligned && off + 16 * K <= B) {
+            uint4 *dst = reinterpret_cast<uint4 *>(out + off);
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4 * K; ++q)
+                for (int b = 0; b < 4; ++b)
+                    if (off + 4 * q + b < B)
+                        out[off + 4 * q + b] = u8(o[q] >> (8 * b));
+        }
+    }
+}
+
+extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
+                                int navail, int32_t *status, const void *gf, hipStream_t st)
+{
+    if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
+        (reinterpret_cast<uintptr_t>(g->parts) & 15))
+        return -ENOSYS;
+    const dim3 grid(g->nstripes);
+    const GfTables *t = (const GfTables *)gf;
+    switch (g->k) {
+#define NKFS_DK(KK, EE)                                                                                     \
+    case KK:                                                                                                \
+        hipLaunchKernelGGL((k_decode_fast<KK, EE>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
+                           status, t);                                                                      \
+        break;
+        NKFS_DK(2, 4)
+        NKFS_DK(3, 4)
+        NKFS_DK(4, 4)
+        NKFS_DK(5, 8)
+        NKFS_DK(6, 8)
+        NKFS_DK(7, 8)
+        NKFS_DK(8, 8)
+#undef NKFS_DK
+    default:
+        return -ENOSYS;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

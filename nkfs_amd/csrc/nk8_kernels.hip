@@ -370,6 +370,8 @@ __global__ __launch_bounds__(256) void k_synth(u8 *blocks, u64 pitch, u32 B, u32
 // ----------------------------------------------------------- launchers
 
 extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, const void *gf, hipStream_t st);
+extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
+                                int32_t *status, const void *gf, hipStream_t st);
 
 static int launch_ok(void)
 {
@@ -431,9 +433,12 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
+    int rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st);
+    if (rc != -ENOSYS)
+        return rc;
     hipLaunchKernelGGL(k_decode_prep, dim3(g->nstripes), dim3(64), 0, st, ids, avail, n_slots, navail, g->k,
                        (u8 *)work, status, (const GfTables *)gf);
-    int rc = launch_ok();
+    rc = launch_ok();
     if (rc)
         return rc;
     const u32 ps = part_size_of(g->block_size, g->k);
