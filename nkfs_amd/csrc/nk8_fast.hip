@@ -174,39 +174,42 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     const u32 nchunks = live ? (v.ps + R - 1) / R : 0;
     const bool aligned = ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
 
+    u32 d[4 * K];
+    auto load_task = [&](u32 r0) {
+        const u64 off = u64(r0) * K;
+        if (aligned && off + 16 * K <= v.B) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const uint4 t = src[q];
+                d[4 * q] = t.x;
+                d[4 * q + 1] = t.y;
+                d[4 * q + 2] = t.z;
+                d[4 * q + 3] = t.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4 * K; ++q) {
+                u32 x = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const u64 p = off + 4 * q + b;
+                    if (p < v.B)
+                        x |= u32(v.blk[p]) << (8 * b);
+                }
+                d[q] = x;
+            }
+        }
+    };
+    if (nchunks && 16 * li < v.ps)
+        load_task(16 * li);
+
     for (u32 c = 0; __any(c < nchunks); ++c) {
         const u32 r0 = c * R + 16 * li;
         if (c < nchunks && r0 < v.ps) {
-            // 16 rows = 16*K input bytes
-            u32 d[4 * K];
-            const u64 off = u64(r0) * K;
-            if (aligned && off + 16 * K <= v.B) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const uint4 t = src[q];
-                    d[4 * q] = t.x;
-                    d[4 * q + 1] = t.y;
-                    d[4 * q + 2] = t.z;
-                    d[4 * q + 3] = t.w;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4 * K; ++q) {
-                    u32 x = 0;
-                    for (int b = 0; b < 4; ++b) {
-                        const u64 p = off + 4 * q + b;
-                        if (p < v.B)
-                            x |= u32(v.blk[p]) << (8 * b);
-                    }
-                    d[q] = x;
-                }
-            }
+            // 16 rows = 16*K input bytes in d[]
             u32 row[16][W];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                constexpr int dummy = 0;
-                (void)dummy;
                 const int p0 = r * K;
                 const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
 #pragma unroll
@@ -226,6 +229,9 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
                     }
                 }
             }
+            // prefetch the next chunk's rows while this one is stored and hashed
+            if (c + 1 < nchunks && r0 + R < v.ps)
+                load_task(r0 + R);
             // rows -> parts: out[i][q] = bytes of part i for rows 4q..4q+3
             u32 out[E][4];
 #pragma unroll
@@ -334,138 +340,168 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
 
 // ------------------------------------------------------------------ decode
 //
-// One wave per stripe, k <= 8 (crt/nk8.c:446-599):
-//  1. lane 0 picks the first k offered parts with distinct ids
+// One wave = G stripes (G = 4 for k <= 4, 2 for k <= 8), k <= 8
+// (crt/nk8.c:446-599):
+//  1. lane 0 of each stripe picks the first k offered parts with distinct ids
 //     (crt/nk8.c:512-537) and forms M(t) = prod_c (t + x_c);
-//  2. lane c < k computes row c of W = V^-1 for V[m][c] = x_c^m in closed
-//     form (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) / M'(x_c)), which
-//     is the unique inverse the reference's Gauss-Jordan produces;
+//  2. lane c < k of the stripe computes row c of W = V^-1 for V[m][c] = x_c^m
+//     in closed form (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) divided
+//     by M'(x_c)), the unique inverse the reference's Gauss-Jordan produces;
 //  3. packed tables U_c[x] = (W[c][0]*x, ..., W[c][k-1]*x) go to LDS;
 //  4. every lane rebuilds 16 rows per step: one 16-byte load from each of the
 //     k parts, k*16 lookups, rows packed back to k*16 contiguous bytes:
 //       block[j*k + m] = XOR_c part_c[j] * W[c][m]      (crt/nk8.c:552-582)
+//     with the next step's loads issued before this step's stores.
 namespace {
 
-struct GfL {
-    uint16_t log[256];
-    u8 exp[768];
-};
+// bit-serial GF(2^8)/0x11B product in registers (no tables needed)
+__device__ inline u32 gfm(u32 a, u32 b)
+{
+    u32 r = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        r ^= a & (0u - ((b >> bit) & 1u));
+        a = ((a << 1) ^ (0x11Bu & (0u - ((a >> 7) & 1u)))) & 0xFFu;
+    }
+    return r;
+}
 
-__device__ inline u8 lmul(const GfL &L, u8 a, u8 b) { return (a && b) ? L.exp[L.log[a] + L.log[b]] : u8(0); }
-__device__ inline u8 ldiv(const GfL &L, u8 a, u8 b) { return (a && b) ? L.exp[L.log[a] + 255 - L.log[b]] : u8(0); }
+__device__ inline u32 gf_inv(u32 a)  // a^254
+{
+    u32 r = 1, x = a;
+#pragma unroll
+    for (int e = 254; e; e >>= 1) {
+        if (e & 1)
+            r = gfm(r, x);
+        x = gfm(x, x);
+    }
+    return r;
+}
 
 }  // namespace
 
 template <int K, int E>
 __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                    int navail, int32_t *status, const GfTables *gft)
+                                                    int navail, int32_t *status)
 {
+    constexpr int G = E == 4 ? 4 : 2;
+    constexpr int LP = 64 / G;
+    constexpr int R = 16 * LP;  // rows per stripe per step
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
-    constexpr int R = 16 * 64;  // rows per step
-    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
-    __shared__ GfL L;
-    __shared__ u8 xs[K], slot[K], M[K + 1], wrow[K][K];
-    __shared__ int have;
+    __shared__ __attribute__((aligned(16))) u8 tbl[G * K * TB];
+    __shared__ u8 slot[G][K], M[G][K + 1], xs[G][K], wrow[G][K][K];
+    __shared__ int have[G];
 
     const int lane = threadIdx.x;
-    const u32 s = blockIdx.x;
-    for (int i = lane; i < 256; i += 64)
-        L.log[i] = gft->log[i];
-    for (int i = lane; i < 768; i += 64)
-        L.exp[i] = gft->exp[i];
-    __syncthreads();
-    if (lane == 0) {
-        const u8 *sid = ids + u64(s) * n_slots;
-        const u8 *sav = avail + u64(s) * navail;
+    const int gi = lane / LP, li = lane % LP;
+    const u32 s = blockIdx.x * G + gi;
+    const bool live = s < g.nstripes;
+    if (li == 0) {
         int h = 0;
-        for (int c = 0; c < navail && h < K; ++c) {
-            const u8 id = sid[sav[c]];
-            bool dup = false;
-            for (int d = 0; d < c; ++d)
-                dup |= sid[sav[d]] == id;
-            if (dup)
-                continue;
-            xs[h] = id;
-            slot[h] = sav[c];
-            ++h;
-        }
-        have = h;
-        if (status)
-            status[s] = h < K ? -EINVAL : 0;
-        if (h == K) {
-            M[0] = 1;
-            for (int c = 0; c < K; ++c) {
-                M[c + 1] = M[c];
-                for (int i = c; i >= 1; --i)
-                    M[i] = M[i - 1] ^ lmul(L, xs[c], M[i]);
-                M[0] = lmul(L, xs[c], M[0]);
+        if (live) {
+            const u8 *sid = ids + u64(s) * n_slots;
+            const u8 *sav = avail + u64(s) * navail;
+            for (int c = 0; c < navail && h < K; ++c) {
+                const u8 sl = sav[c];
+                const u8 id = sid[sl];
+                bool dup = false;
+                for (int d = 0; d < h; ++d)
+                    dup |= xs[gi][d] == id;
+                if (dup)
+                    continue;
+                xs[gi][h] = id;
+                slot[gi][h] = sl;
+                ++h;
             }
+            if (status)
+                status[s] = h < K ? -EINVAL : 0;
+        }
+        have[gi] = h;
+        if (h == K) {
+            u32 m[K + 1];
+            m[0] = 1;
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const u32 x = xs[gi][c];
+                m[c + 1] = m[c];
+#pragma unroll
+                for (int i = c; i >= 1; --i)
+                    m[i] = m[i - 1] ^ gfm(x, m[i]);
+                m[0] = gfm(x, m[0]);
+            }
+#pragma unroll
+            for (int i = 0; i <= K; ++i)
+                M[gi][i] = u8(m[i]);
         }
     }
     __syncthreads();
-    if (have < K)
-        return;
-    if (lane < K) {
-        const u8 xc = xs[lane];
-        u8 q[K];
-        u8 acc = M[K];
+    const bool ok = have[gi] == K;
+    if (ok && li < K) {
+        const u32 xc = xs[gi][li];
+        u32 q[K];
+        u32 acc = M[gi][K];
         q[K - 1] = acc;
 #pragma unroll
         for (int i = K - 1; i >= 1; --i) {
-            acc = M[i] ^ lmul(L, xc, acc);
+            acc = M[gi][i] ^ gfm(xc, acc);
             q[i - 1] = acc;
         }
-        u8 d = 0;
+        u32 d = 0;
 #pragma unroll
         for (int i = K - 1; i >= 0; --i)
-            d = lmul(L, d, xc) ^ q[i];
+            d = gfm(d, xc) ^ q[i];
+        const u32 dinv = gf_inv(d);
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            wrow[lane][i] = ldiv(L, q[i], d);
+            wrow[gi][li][i] = u8(gfm(q[i], dinv));
     }
     __syncthreads();
-    // packed tables U_c, entries x = lane, lane+64, ...
+    u8 *mytbl = tbl + gi * K * TB;
+    if (ok) {
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-        u32 basis[8][W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            u32 x = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (4 * w + b < K)
-                    x |= u32(wrow[c][4 * w + b]) << (8 * b);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                basis[b][w] = x;
-                x = gf_xtime4(x);
-            }
-        }
-        for (int x = lane; x < 256; x += 64) {
+        for (int c = 0; c < K; ++c) {
+            u32 basis[8][W];
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                u32 e = 0;
+                u32 x = 0;
 #pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
-                *reinterpret_cast<u32 *>(tbl + c * TB + x * E + 4 * w) = e;
+                for (int b = 0; b < 4; ++b)
+                    if (4 * w + b < K)
+                        x |= u32(wrow[gi][c][4 * w + b]) << (8 * b);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    basis[b][w] = x;
+                    x = gf_xtime4(x);
+                }
+            }
+            for (int x = li; x < 256; x += LP) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    u32 e = 0;
+#pragma unroll
+                    for (int b = 0; b < 8; ++b)
+                        e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
+                    *reinterpret_cast<u32 *>(mytbl + c * TB + x * E + 4 * w) = e;
+                }
             }
         }
     }
     __syncthreads();
+    if (!ok)
+        return;
 
     const u32 B = g.block_size;
     const u32 ps = part_size_of(B, K);
     const u8 *src[K];
 #pragma unroll
     for (int c = 0; c < K; ++c)
-        src[c] = g.parts + (u64(s) * n_slots + slot[c]) * g.part_pitch;
+        src[c] = g.parts + (u64(s) * n_slots + slot[gi][c]) * g.part_pitch;
     u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
     const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
 
-    for (u32 r0 = 16 * lane; r0 < ps; r0 += R) {
-        u32 pv[K][4];
+    u32 pv[K][4];
+    auto load_step = [&](u32 r0) {
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
@@ -474,6 +510,11 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
             pv[c][2] = t.z;
             pv[c][3] = t.w;
         }
+    };
+    u32 r0 = 16 * li;
+    if (r0 < ps)
+        load_step(r0);
+    for (; r0 < ps; r0 += R) {
         u32 row[16][W];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -483,7 +524,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
             for (int c = 0; c < K; ++c) {
                 const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                const u8 *e = tbl + c * TB + byte * E;
+                const u8 *e = mytbl + c * TB + byte * E;
                 if constexpr (E == 8) {
                     const uint2 t = *reinterpret_cast<const uint2 *>(e);
                     row[r][0] ^= t.x;
@@ -493,6 +534,8 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                 }
             }
         }
+        if (r0 + R < ps)
+            load_step(r0 + R);  // prefetch the next step under this one's stores
         // pack 16 rows of K bytes into 4*K dwords (byte p = r*K + m)
         u32 o[4 * K];
 #pragma unroll
@@ -523,18 +566,18 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 }
 
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *gf, hipStream_t st)
+                                int navail, int32_t *status, const void *, hipStream_t st)
 {
     if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
         return -ENOSYS;
-    const dim3 grid(g->nstripes);
-    const GfTables *t = (const GfTables *)gf;
+    const int G = g->k <= 4 ? 4 : 2;
+    const dim3 grid((g->nstripes + G - 1) / G);
     switch (g->k) {
 #define NKFS_DK(KK, EE)                                                                                     \
     case KK:                                                                                                \
         hipLaunchKernelGGL((k_decode_fast<KK, EE>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
-                           status, t);                                                                      \
+                           status);                                                                         \
         break;
         NKFS_DK(2, 4)
         NKFS_DK(3, 4)

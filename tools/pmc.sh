@@ -1,0 +1,14 @@
+#!/bin/bash
+# HBM traffic per kernel from PMC counters, one counter per pass (FETCH_SIZE
+# and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md §rocprofv3).
+#   bash tools/pmc.sh <config>
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+c=${1:-c2}
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc_${c}_$ctr -o run -- \
+    python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > gpurun_out/pmc_${c}_$ctr.log 2>&1 \
+    || { echo "pmc $ctr failed"; tail -20 gpurun_out/pmc_${c}_$ctr.log; exit 1; }
+done
+python3 tools/pmc_summary.py gpurun_out/pmc_${c}_FETCH_SIZE gpurun_out/pmc_${c}_WRITE_SIZE | tee gpurun_out/pmc_${c}_summary.txt
