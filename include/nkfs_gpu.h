@@ -38,7 +38,9 @@ int nkfs_gpu_ready(void);
 
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */
 uint32_t nkfs_part_size(uint32_t block_size, int k);
-/* part_size rounded up to 16 bytes: the pitch ragged batches use. */
+/* part_size rounded up to 256 bytes: the pitch ragged batches and the
+ * drop-in entry points use, and the recommended pitch for uniform batches
+ * (every chunk the encoder writes then covers whole cache lines). */
 uint64_t nkfs_part_pitch(uint32_t block_size, int k);
 
 /* Encode (+ XXH64 of every part when d_digests != NULL) a uniform batch.

@@ -98,7 +98,7 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 		return -EIO;
 	int err;
 	uint32_t ps = nkfs_part_size(B, k);
-	uint64_t pitch = round16(ps);
+	uint64_t pitch = nkfs_part_pitch(B, k);
 	uint64_t off_parts = round16(B), off_ids = off_parts + pitch * (uint64_t)n;
 	void *dv;
 	if ((err = nkfs_ctx_dev(c, off_ids + round16((uint64_t)n), &dv)))
@@ -176,7 +176,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 		return -EIO;
 	int err;
 	uint32_t ps = nkfs_part_size(block_size, k);
-	uint64_t pitch = round16(ps);
+	uint64_t pitch = nkfs_part_pitch(block_size, k);
 	uint64_t off_parts = 0;
 	uint64_t off_ids = off_parts + pitch * (uint64_t)k;
 	uint64_t off_avail = off_ids + 256;

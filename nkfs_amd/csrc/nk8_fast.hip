@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gf256.h"
 #include "nkfs_internal.h"
@@ -89,7 +90,7 @@ __device__ inline Stripe stripe_at(const nkfs_geom &g, u32 s)
         v.blk = g.blocks + g.block_off[s];
         v.parts = g.parts + g.part_off[s];
         v.ps = part_size_of(v.B, g.k);
-        v.pitch = (u64(v.ps) + 15) & ~u64(15);
+        v.pitch = (u64(v.ps) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
     } else {
         v.B = g.block_size;
         v.blk = g.blocks + u64(s) * g.block_pitch;
@@ -203,11 +204,17 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     if (nchunks && 16 * li < v.ps)
         load_task(16 * li);
 
-    for (u32 c = 0; __any(c < nchunks); ++c) {
+    // Software pipeline: iteration c encodes chunk c while the hash lanes run
+    // the XXH64 rounds of chunk c-1 from registers (hw[]), so the serial
+    // multiply chain overlaps the table lookups instead of following them.
+    constexpr int RPC = R / 32;  // rounds per chain per chunk
+    u64 hw[RPC];
+    int hvalid = 0;              // rounds pending in hw[]
+    for (u32 c = 0; __any(nchunks && c <= nchunks); ++c) {
         const u32 r0 = c * R + 16 * li;
-        if (c < nchunks && r0 < v.ps) {
-            // 16 rows = 16*K input bytes in d[]
-            u32 row[16][W];
+        const bool act = c < nchunks && r0 < v.ps;
+        u32 row[16][W];
+        if (act) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int p0 = r * K;
@@ -229,7 +236,16 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
                     }
                 }
             }
-            // prefetch the next chunk's rows while this one is stored and hashed
+        }
+        if constexpr (HASH) {
+#pragma unroll
+            for (int rr = 0; rr < RPC; ++rr) {
+                const u64 nxt = xxh_round(acc, hw[rr]);
+                acc = rr < hvalid ? nxt : acc;
+            }
+        }
+        if (act) {
+            // prefetch the next chunk's rows while this one is stored
             if (c + 1 < nchunks && r0 + R < v.ps)
                 load_task(r0 + R);
             // rows -> parts: out[i][q] = bytes of part i for rows 4q..4q+3
@@ -258,16 +274,18 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
         }
         if constexpr (HASH) {
             __syncthreads();
+            hvalid = 0;
             if (hlane && c < nchunks) {
                 const u8 *src = xbuf + (gi * E + hi) * SP + 8 * ha;
-                const u32 first = c * (R / 32);
-#pragma unroll 4
-                for (int rr = 0; rr < R / 32; ++rr) {
-                    if (first + rr < nst)
-                        acc = xxh_round(acc, *reinterpret_cast<const u64 *>(src + 32 * rr));
-                }
+                const int left = int(nst) - int(c * RPC);
+                hvalid = left < 0 ? 0 : (left > RPC ? RPC : left);
+#pragma unroll
+                for (int rr = 0; rr < RPC; ++rr)
+                    hw[rr] = *reinterpret_cast<const u64 *>(src + 32 * rr);
             }
             __syncthreads();
+        } else if (c >= nchunks) {
+            break;
         }
     }
 

@@ -28,7 +28,7 @@ __host__ __device__ inline u32 part_size_of(u32 block_size, int k)
 
 __host__ __device__ inline u64 pitch_of(u32 block_size, int k)
 {
-    return (u64(part_size_of(block_size, k)) + 15) & ~u64(15);
+    return (u64(part_size_of(block_size, k)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
 }
 
 struct StripeView {

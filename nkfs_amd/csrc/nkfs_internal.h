@@ -51,6 +51,11 @@ int nkfs_launch_synth(uint8_t *blocks, uint64_t block_pitch,
 		      uint32_t block_size, uint32_t nstripes,
 		      uint64_t seed, uint64_t first_stripe, void *stream);
 
+/* Part pitch used when the library lays parts out itself (ragged batches,
+ * the drop-in entry points): part_size rounded up to whole 256-byte spans so
+ * that every chunk a kernel writes covers full 128-byte cache lines. */
+#define NKFS_PART_ALIGN 256u
+
 /* Sizes shared by host and launchers. */
 uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k);
 size_t nkfs_gf_tables_bytes(void);

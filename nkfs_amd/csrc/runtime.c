@@ -207,7 +207,7 @@ uint32_t nkfs_part_size(uint32_t block_size, int k)
 
 uint64_t nkfs_part_pitch(uint32_t block_size, int k)
 {
-	return ((uint64_t)nkfs_part_size(block_size, k) + 15) & ~(uint64_t)15;
+	return ((uint64_t)nkfs_part_size(block_size, k) + NKFS_PART_ALIGN - 1) & ~(uint64_t)(NKFS_PART_ALIGN - 1);
 }
 
 /* crt/nk8.c:356-360: 2 <= k <= n <= 255, k <= 254, block_size > 0 */

@@ -78,6 +78,6 @@ def test_no_gpu_fails_loudly():
 def test_part_geometry():
     L = _lib.lib()
     assert L.nkfs_part_size(1048576, 5) == 209716
-    assert L.nkfs_part_pitch(1048576, 5) == 209728
+    assert L.nkfs_part_pitch(1048576, 5) == 209920
     assert L.nkfs_part_size(4096, 2) == 2048
-    assert L.nkfs_part_pitch(1, 2) == 16
+    assert L.nkfs_part_pitch(1, 2) == 256

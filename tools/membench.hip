@@ -39,6 +39,23 @@ __global__ void k_r1w2(const uint4 *__restrict__ a, uint4 *__restrict__ b, uint4
     }
 }
 
+// each lane reads K consecutive 16-byte pieces (K*16 B per lane, stride K*16
+// across lanes) -- the encode's per-lane row-block load for k = K
+template <int K>
+__global__ void k_read_lane_contig(const uint4 *__restrict__ a, size_t n, uint4 *sink)
+{
+    uint4 acc = {0, 0, 0, 0};
+    const size_t tasks = n / K;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tasks; t += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            uint4 v = a[t * K + q];
+            acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = acc;
+}
+
 int main()
 {
     const size_t bytes = (size_t)1 << 30;
@@ -73,6 +90,25 @@ int main()
             double moved = kind == 0 ? bytes : kind == 1 ? bytes : kind == 2 ? 2.0 * bytes : 1.5 * bytes;
             const char *nm[] = {"read", "write", "copy 1:1", "read1:write2"};
             printf("grid %5d  %-13s %7.1f GB/s\n", grid, nm[kind], moved / best / 1e6);
+        }
+    }
+    for (int gi = 0; gi < 5; ++gi) {
+        int grid = grids[gi];
+        for (int kind = 0; kind < 3; ++kind) {
+            float best = 1e9;
+            for (int rep = 0; rep < 6; ++rep) {
+                hipEventRecord(e0);
+                if (kind == 0) hipLaunchKernelGGL(k_read_lane_contig<2>, grid, 64, 0, 0, a, n, c);
+                if (kind == 1) hipLaunchKernelGGL(k_read_lane_contig<5>, grid, 64, 0, 0, a, n, c);
+                if (kind == 2) hipLaunchKernelGGL(k_read_lane_contig<1>, grid, 64, 0, 0, a, n, c);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms;
+                hipEventElapsedTime(&ms, e0, e1);
+                if (rep && ms < best) best = ms;
+            }
+            const char *nm[] = {"read 32B/lane", "read 80B/lane", "read 16B/lane"};
+            printf("grid %5d x64  %-13s %7.1f GB/s\n", grid, nm[kind], bytes / best / 1e6);
         }
     }
     return 0;
