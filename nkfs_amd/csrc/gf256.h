@@ -46,9 +46,11 @@ NKFS_HD inline constexpr uint32_t gf_xtime4(uint32_t v)
 //   exp[510..767] = 0 so that exp[LOG_ZERO + anything <= 257] == 0.
 //   log[x] = discrete log of x (x != 0); log[0] = LOG_ZERO.
 constexpr int LOG_ZERO = 510;
+//   inv[x] = x^-1 (inv[0] = 0).
 struct GfTables {
     uint16_t log[256];
     uint8_t exp[768];
+    uint8_t inv[256];
 };
 
 }  // namespace nkfs

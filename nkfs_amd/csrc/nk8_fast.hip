@@ -53,6 +53,56 @@ __device__ inline u32 gf_mul_packed(u32 a, u32 b)
     return r;
 }
 
+// Fill a 256-entry packed product table T[x] = XOR_{bit b of x} basis[b]
+// (multiplication by a constant is GF(2)-linear) with the LP lanes of one
+// stripe: lane li owns entries x = li + LP*j, walks j in Gray-code order and
+// pays one XOR per entry and word; consecutive lanes write consecutive
+// entries, so the LDS stores are conflict-free.
+template <int W, int LP>
+__device__ inline void build_table(u8 *t, const u32 (&basis)[8][W], int li)
+{
+    constexpr int LB = LP == 16 ? 4 : 5;
+    static_assert(LP == 16 || LP == 32, "lanes per stripe");
+    u32 hv[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        u32 e = 0;
+#pragma unroll
+        for (int b = 0; b < LB; ++b)
+            e ^= basis[b][w] & (0u - ((u32(li) >> b) & 1u));
+        hv[w] = e;
+    }
+#pragma unroll
+    for (int j = 0; j < 256 / LP; ++j) {
+        if (j) {
+            const int bit = __builtin_ctz(j);
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                hv[w] ^= basis[LB + bit][w];
+        }
+        const int x = li + LP * (j ^ (j >> 1));
+        if constexpr (W == 2)
+            *reinterpret_cast<uint2 *>(t + x * 8) = make_uint2(hv[0], hv[1]);
+        else
+            *reinterpret_cast<u32 *>(t + x * 4) = hv[0];
+    }
+}
+
+// basis[b] = packed coefficient row * 2^b (b = 0..7)
+template <int W>
+__device__ inline void make_basis(u32 (&basis)[8][W], const u32 (&row)[W])
+{
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        u32 x = row[w];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            basis[b][w] = x;
+            x = gf_xtime4(x);
+        }
+    }
+}
+
 // 4x4 byte transpose: in[r] byte c -> out[c] byte r
 __device__ inline void transpose4(u32 a, u32 b, u32 c, u32 d, u32 &o0, u32 &o1, u32 &o2, u32 &o3)
 {
@@ -142,25 +192,8 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
 #pragma unroll
     for (int m = 1; m < K; ++m) {
         u32 basis[8][W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            u32 x = coef[w];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                basis[b][w] = x;
-                x = gf_xtime4(x);
-            }
-        }
-        for (int x = li; x < 256; x += LP) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                u32 e = 0;
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
-                *reinterpret_cast<u32 *>(mytbl + (m - 1) * TB + x * E + 4 * w) = e;
-            }
-        }
+        make_basis<W>(basis, coef);
+        build_table<W, LP>(mytbl + (m - 1) * TB, basis, li);
 #pragma unroll
         for (int w = 0; w < W; ++w)
             coef[w] = gf_mul_packed(coef[w], idw[w]);
@@ -384,23 +417,11 @@ __device__ inline u32 gfm(u32 a, u32 b)
     return r;
 }
 
-__device__ inline u32 gf_inv(u32 a)  // a^254
-{
-    u32 r = 1, x = a;
-#pragma unroll
-    for (int e = 254; e; e >>= 1) {
-        if (e & 1)
-            r = gfm(r, x);
-        x = gfm(x, x);
-    }
-    return r;
-}
-
 }  // namespace
 
 template <int K, int E>
 __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                    int navail, int32_t *status)
+                                                    int navail, int32_t *status, const u8 *inv)
 {
     constexpr int G = E == 4 ? 4 : 2;
     constexpr int LP = 64 / G;
@@ -409,20 +430,37 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     constexpr int TB = 256 * E;
     __shared__ __attribute__((aligned(16))) u8 tbl[G * K * TB];
     __shared__ u8 slot[G][K], M[G][K + 1], xs[G][K], wrow[G][K][K];
+    __shared__ u8 cand_id[G][LP], cand_slot[G][LP];
+    __shared__ u32 inv4[64];  // GF inverses, 4 per word
     __shared__ int have[G];
 
     const int lane = threadIdx.x;
     const int gi = lane / LP, li = lane % LP;
     const u32 s = blockIdx.x * G + gi;
     const bool live = s < g.nstripes;
+    inv4[lane] = reinterpret_cast<const u32 *>(inv)[lane];
+    // the first LP offered parts and their ids, loaded in parallel
+    const u8 *sid = ids + u64(s) * n_slots;
+    const u8 *sav = avail + u64(s) * navail;
+    if (live && li < navail) {
+        const u8 sl = sav[li];
+        cand_slot[gi][li] = sl;
+        cand_id[gi][li] = sid[sl];
+    }
+    __syncthreads();
     if (li == 0) {
         int h = 0;
         if (live) {
-            const u8 *sid = ids + u64(s) * n_slots;
-            const u8 *sav = avail + u64(s) * navail;
+            // first K distinct ids in offered order (crt/nk8.c:512-537)
             for (int c = 0; c < navail && h < K; ++c) {
-                const u8 sl = sav[c];
-                const u8 id = sid[sl];
+                u8 sl, id;
+                if (c < LP) {
+                    sl = cand_slot[gi][c];
+                    id = cand_id[gi][c];
+                } else {
+                    sl = sav[c];
+                    id = sid[sl];
+                }
                 bool dup = false;
                 for (int d = 0; d < h; ++d)
                     dup |= xs[gi][d] == id;
@@ -469,7 +507,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
         for (int i = K - 1; i >= 0; --i)
             d = gfm(d, xc) ^ q[i];
-        const u32 dinv = gf_inv(d);
+        const u32 dinv = (inv4[d >> 2] >> (8 * (d & 3))) & 0xFFu;
 #pragma unroll
         for (int i = 0; i < K; ++i)
             wrow[gi][li][i] = u8(gfm(q[i], dinv));
@@ -479,7 +517,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     if (ok) {
 #pragma unroll
         for (int c = 0; c < K; ++c) {
-            u32 basis[8][W];
+            u32 rw[W];
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 u32 x = 0;
@@ -487,22 +525,11 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                 for (int b = 0; b < 4; ++b)
                     if (4 * w + b < K)
                         x |= u32(wrow[gi][c][4 * w + b]) << (8 * b);
-#pragma unroll
-                for (int b = 0; b < 8; ++b) {
-                    basis[b][w] = x;
-                    x = gf_xtime4(x);
-                }
+                rw[w] = x;
             }
-            for (int x = li; x < 256; x += LP) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    u32 e = 0;
-#pragma unroll
-                    for (int b = 0; b < 8; ++b)
-                        e ^= basis[b][w] & (0u - ((u32(x) >> b) & 1u));
-                    *reinterpret_cast<u32 *>(mytbl + c * TB + x * E + 4 * w) = e;
-                }
-            }
+            u32 basis[8][W];
+            make_basis<W>(basis, rw);
+            build_table<W, LP>(mytbl + c * TB, basis, li);
         }
     }
     __syncthreads();
@@ -584,18 +611,19 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 }
 
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *, hipStream_t st)
+                                int navail, int32_t *status, const void *gf, hipStream_t st)
 {
     if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
         return -ENOSYS;
     const int G = g->k <= 4 ? 4 : 2;
     const dim3 grid((g->nstripes + G - 1) / G);
+    const GfTables *t = (const GfTables *)gf;
     switch (g->k) {
 #define NKFS_DK(KK, EE)                                                                                     \
     case KK:                                                                                                \
         hipLaunchKernelGGL((k_decode_fast<KK, EE>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
-                           status);                                                                         \
+                           status, t->inv);                                                                 \
         break;
         NKFS_DK(2, 4)
         NKFS_DK(3, 4)

@@ -107,6 +107,9 @@ __global__ void k_gf_init(GfTables *t)
     for (int i = 510; i < 768; ++i)
         t->exp[i] = 0;
     t->log[0] = LOG_ZERO;
+    t->inv[0] = 0;
+    for (int a = 1; a < 256; ++a)
+        t->inv[a] = t->exp[255 - t->log[a]];
 }
 
 // ------------------------------------------------------ generic encode
