@@ -129,9 +129,19 @@ def main():
     work = batch.decode_workspace(S, k, device)
     status = torch.empty(S, dtype=torch.int32, device=device)
 
-    def step():
+    # HIP events around every launch of the timed region, on the stream the
+    # library launches on (torch's current stream): per-kernel live timing
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(e=None):
+        if e:
+            e[0].record(stream)
         batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream)
+        if e:
+            e[1].record(stream)
         batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status, stream=stream)
+        if e:
+            e[2].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -139,12 +149,14 @@ def main():
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(ev[i])
     torch.cuda.synchronize(device)
     barrier()
     t1 = time.perf_counter()
     elapsed = reduce_max(t1 - t0, device)
+    enc_s = sum(e[0].elapsed_time(e[1]) for e in ev) / 1e3 / args.steps
+    dec_s = sum(e[1].elapsed_time(e[2]) for e in ev) / 1e3 / args.steps
 
     # correctness of what was timed: decode == input, digests vs oracle sample
     ok = bool(torch.equal(out, blocks[:, :B])) and int(status.abs().sum()) == 0
@@ -158,23 +170,6 @@ def main():
     for d in dig:
         dx ^= d
     gathered = gather_digest_xor(dx, device)
-
-    # dominant kernel: encode(+hash) alone, HIP events on the launch stream
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    reps = max(5, args.steps)
-    ev0.record(stream)
-    for _ in range(reps):
-        batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    enc_s = ev0.elapsed_time(ev1) / 1e3 / reps
-    ev0.record(stream)
-    for _ in range(reps):
-        batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status, stream=stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    dec_s = ev0.elapsed_time(ev1) / 1e3 / reps
     enc_bytes = S * (B + n * ps + 8 * n)
     dec_bytes = S * (k * ps + B + k)
 
@@ -202,7 +197,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(enc_bytes / enc_s / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(args.config),
             "bytes_per_launch": enc_bytes,
             "us_per_launch": round(enc_s * 1e6, 2),
         },
@@ -222,25 +217,43 @@ def main():
         dist.destroy_process_group()
 
 
+def pmc_traffic(config):
+    """Per-launch HBM bytes of the encode kernel from the committed rocprofv3
+    PMC summary (tools/pmc.sh: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    FETCH_SIZE halving corrected per MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            entry = json.load(f).get(config)
+        return None if entry is None else entry["encode_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(S, B, n, k, target_s):
     """The reference's own split + XXH64 + assemble (oracle/_ref), on a
-    bounded sample of this workload, on the host cores of this box."""
+    bounded sample of this workload (at most S stripes, reused across
+    passes until ~target_s seconds of CPU time), on this box's host cores."""
     from nkfs_amd import synth
     from oracle import oracle as O
     kind = "reference" if O.ref_lib() is not None else "port"
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    probe = min(S, max(16, (1 << 22) // B))
-    blocks = synth.batch_bytes(probe, B)
-    sv = synth.batch_survivors(probe, n, k)
-    secs, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
-    count = int(min(S * 4, max(probe, probe * target_s / max(secs, 1e-6))))
-    count = max(threads, min(count, (2 << 30) // B))
+    count = int(max(threads, min(S, (256 << 20) // B)))
     blocks = synth.batch_bytes(count, B)
     sv = synth.batch_survivors(count, n, k)
-    secs, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
-    return {"value": round(count * B / secs / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{count} stripes x {B} B (N={n},K={k}): nk8_split_block + XXH64 of every part + "
-                      f"nk8_assemble_block from {k} survivors, {threads} pthreads, {secs:.1f} s"}
+    secs, _ = O.bench_encode_decode(blocks[: max(threads, count // 16)], n, k, sv[: max(threads, count // 16)],
+                                    threads, kind)
+    per_stripe = secs / max(threads, count // 16)
+    passes = max(1, int(round(target_s / max(per_stripe * count, 1e-9))))
+    total = 0.0
+    for _ in range(passes):
+        t, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
+        total += t
+    done = count * passes
+    return {"value": round(done * B / total / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{passes} pass(es) over {count} stripes x {B} B (N={n},K={k}): nk8_split_block + "
+                      f"XXH64 of every part + nk8_assemble_block from {k} survivors, {threads} pthreads, "
+                      f"{total:.1f} s"}
 
 
 def pcie_rate(batch, blocks_np, S, B, n, k, ids, avail, device, stream):

@@ -1,0 +1,60 @@
+"""Multi-rank plumbing of bench.py on CPU (gloo, world size 2): weak-scaling
+stripe partition, max-over-ranks timing, digest all-gather.  The GPU run uses
+the same functions over RCCL (backend "nccl") with one process per GPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    r, w, local = bench.dist_setup("gloo")
+    dev = torch.device("cpu")
+    first, count = bench.stripe_range(r, 65536)
+    t = bench.reduce_max(1.0 + r, dev)
+    xs = bench.gather_digest_xor((0xF000_0000_0000_0000 | r), dev)
+    bench.barrier()
+    q.put((r, w, local, first, count, t, xs))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    for r, (rank, world, local, first, count, t, xs) in enumerate(res):
+        assert (rank, world, local) == (r, 2, r)
+        assert (first, count) == (r * 65536, 65536)  # disjoint stripe ranges, fixed per-GPU work
+        assert t == 2.0                              # max over ranks
+        assert xs == [0xF000_0000_0000_0000, 0xF000_0000_0000_0001]
+
+
+def test_single_rank_defaults(monkeypatch):
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.dist_setup("gloo") == (0, 1, 0)
+    assert bench.reduce_max(3.5, torch.device("cpu")) == 3.5
+    assert bench.gather_digest_xor(7, torch.device("cpu")) == [7]

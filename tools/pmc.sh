@@ -11,4 +11,4 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
     python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu > gpurun_out/pmc_${c}_$ctr.log 2>&1 \
     || { echo "pmc $ctr failed"; tail -20 gpurun_out/pmc_${c}_$ctr.log; exit 1; }
 done
-python3 tools/pmc_summary.py gpurun_out/pmc_${c}_FETCH_SIZE gpurun_out/pmc_${c}_WRITE_SIZE | tee gpurun_out/pmc_${c}_summary.txt
+python3 tools/pmc_summary.py gpurun_out/pmc_${c}_FETCH_SIZE gpurun_out/pmc_${c}_WRITE_SIZE --json gpurun_out/traffic.json --config $c | tee gpurun_out/pmc_${c}_summary.txt

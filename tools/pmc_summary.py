@@ -1,12 +1,17 @@
 """Summarise rocprofv3 --pmc CSVs: mean counter value per kernel name.
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
-reports half the bytes of a wide coalesced streaming read
-(MI355X_MICROARCH.md §HBM), so the summary also prints 2x FETCH_SIZE."""
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR [--json out.json --config c2]
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md §HBM),
+so HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE; --json records that
+for the encode and decode kernels under the config name (bench.py reads it
+as roofline.traffic)."""
+import argparse
 import csv
 import glob
+import json
 import os
-import sys
 from collections import defaultdict
 
 
@@ -18,13 +23,31 @@ def load(d):
     return vals
 
 
+ap = argparse.ArgumentParser()
+ap.add_argument("dirs", nargs="+")
+ap.add_argument("--json")
+ap.add_argument("--config")
+a = ap.parse_args()
 out = {}
-for d in sys.argv[1:]:
+for d in a.dirs:
     for (k, c), v in load(d).items():
         out.setdefault(k, {})[c] = sum(v) / len(v)
+rec = {}
 for k, cs in sorted(out.items(), key=lambda kv: -sum(kv[1].values())):
     if not any(s in k for s in ("k_encode", "k_decode", "k_hash", "k_xxh", "k_synth")):
         continue
     f = cs.get("FETCH_SIZE", 0) * 1024
     w = cs.get("WRITE_SIZE", 0) * 1024
     print(f"{k[:70]:70s} FETCH {f/1e6:10.1f} MB (x2 {2*f/1e6:10.1f})  WRITE {w/1e6:10.1f} MB")
+    for kind in ("encode", "decode"):
+        if f"k_{kind}" in k and f"{kind}_bytes_per_launch" not in rec:
+            rec[f"{kind}_kernel"] = k
+            rec[f"{kind}_bytes_per_launch"] = int(2 * f + w)
+            rec[f"{kind}_fetch_size_x2"] = int(2 * f)
+            rec[f"{kind}_write_size"] = int(w)
+if a.json and a.config:
+    doc = {}
+    if os.path.exists(a.json):
+        doc = json.load(open(a.json))
+    doc[a.config] = rec
+    json.dump(doc, open(a.json, "w"), indent=1, sort_keys=True)
