@@ -61,8 +61,8 @@ __device__ inline u32 gf_mul_packed(u32 a, u32 b)
 template <int W, int LP>
 __device__ inline void build_table(u8 *t, const u32 (&basis)[8][W], int li)
 {
-    constexpr int LB = LP == 16 ? 4 : 5;
-    static_assert(LP == 16 || LP == 32, "lanes per stripe");
+    constexpr int LB = LP == 16 ? 4 : LP == 32 ? 5 : 6;
+    static_assert(LP == 16 || LP == 32 || LP == 64, "lanes per stripe");
     u32 hv[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -101,6 +101,61 @@ __device__ inline void make_basis(u32 (&basis)[8][W], const u32 (&row)[W])
             x = gf_xtime4(x);
         }
     }
+}
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+// 16-byte store, plain or non-temporal (global_store_dwordx4 ... nt): the
+// parts/blocks are written once and not read again by this kernel
+__device__ inline void store16(void *p, u32 a, u32 b, u32 c, u32 d, bool nt)
+{
+    const v4u v = {a, b, c, d};
+    if (nt)
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+    else
+        *reinterpret_cast<v4u *>(p) = v;
+}
+
+// Output dword q (bytes 4q..4q+3) of 4 consecutive K-byte rows, each row
+// held in W dwords of `row` (row r, byte m at row[r*W + m/4] byte m%4).
+// The <= 3 distinct source dwords are merged with one or two v_perm_b32.
+template <int K, int W>
+__device__ __forceinline__ u32 pack_dword(const u32 *row, int q)
+{
+    int src[4], byt[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int p = 4 * q + b, r = p / K, m = p % K;
+        src[b] = r * W + (m >> 2);
+        byt[b] = m & 3;
+    }
+    // distinct sources in first-use order
+    int d0 = src[0], d1 = -1, d2 = -1;
+#pragma unroll
+    for (int b = 1; b < 4; ++b) {
+        if (src[b] != d0 && d1 < 0)
+            d1 = src[b];
+        else if (src[b] != d0 && src[b] != d1 && d2 < 0)
+            d2 = src[b];
+    }
+    u32 sel = 0;
+    if (d1 < 0) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            sel |= u32(byt[b]) << (8 * b);
+        return __builtin_amdgcn_perm(row[d0], row[d0], sel);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        sel |= u32(src[b] == d0 ? byt[b] : 4 + byt[b]) << (8 * b);
+    const u32 t = __builtin_amdgcn_perm(row[d1], row[d0], sel);
+    if (d2 < 0)
+        return t;
+    u32 sel2 = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        sel2 |= u32(src[b] == d2 ? 4 + byt[b] : b) << (8 * b);
+    return __builtin_amdgcn_perm(row[d2], t, sel2);
 }
 
 // 4x4 byte transpose: in[r] byte c -> out[c] byte r
@@ -154,7 +209,7 @@ __device__ inline Stripe stripe_at(const nkfs_geom &g, u32 s)
 }  // namespace
 
 template <int K, int E, bool HASH>
-__global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, u64 *digests)
+__global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
     constexpr int G = E == 4 ? 4 : 2;   // stripes per wave
     constexpr int LP = 64 / G;          // lanes per stripe
@@ -295,7 +350,7 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
                     const uint4 val = make_uint4(out[i][0], out[i][1], out[i][2], out[i][3]);
                     u8 *dst = v.parts + u64(i) * v.pitch + r0;
                     if (aligned) {
-                        *reinterpret_cast<uint4 *>(dst) = val;
+                        store16(dst, val.x, val.y, val.z, val.w, nt);
                     } else {
                         for (int b = 0; b < 16 && r0 + b < v.ps; ++b)
                             dst[b] = u8(out[i][b >> 2] >> (8 * (b & 3)));
@@ -344,13 +399,20 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     }
 }
 
+// NKFS_STORE_NT=0/1 overrides the default store flavour (tuning knob)
+static bool store_nt()
+{
+    const char *e = getenv("NKFS_STORE_NT");
+    return e ? atoi(e) != 0 : false;
+}
+
 template <int E, bool HASH>
-static int launch_k(int k, dim3 grid, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig)
+static int launch_k(int k, dim3 grid, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
 {
     switch (k) {
 #define NKFS_K(KK)                                                                        \
     case KK:                                                                              \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, HASH>), grid, dim3(64), 0, st, g, ids, dig); \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, HASH>), grid, dim3(64), 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -377,13 +439,14 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     const int E = g->n <= 4 ? 4 : 8;
     const int G = E == 4 ? 4 : 2;
     const dim3 grid((g->nstripes + G - 1) / G);
+    const bool nt = store_nt();
     int rc;
     if (E == 4)
-        rc = digests ? launch_k<4, true>(g->k, grid, st, *g, ids, digests)
-                     : launch_k<4, false>(g->k, grid, st, *g, ids, digests);
+        rc = digests ? launch_k<4, true>(g->k, grid, st, *g, ids, digests, nt)
+                     : launch_k<4, false>(g->k, grid, st, *g, ids, digests, nt);
     else
-        rc = digests ? launch_k<8, true>(g->k, grid, st, *g, ids, digests)
-                     : launch_k<8, false>(g->k, grid, st, *g, ids, digests);
+        rc = digests ? launch_k<8, true>(g->k, grid, st, *g, ids, digests, nt)
+                     : launch_k<8, false>(g->k, grid, st, *g, ids, digests, nt);
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -419,11 +482,11 @@ __device__ inline u32 gfm(u32 a, u32 b)
 
 }  // namespace
 
-template <int K, int E>
-__global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                    int navail, int32_t *status, const u8 *inv)
+template <int K, int E, int G, int MINW>
+__global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
+                                                          int navail, int32_t *status, const u8 *inv, bool nt,
+                                                          int slices)
 {
-    constexpr int G = E == 4 ? 4 : 2;
     constexpr int LP = 64 / G;
     constexpr int R = 16 * LP;  // rows per stripe per step
     constexpr int W = E / 4;
@@ -436,7 +499,10 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 
     const int lane = threadIdx.x;
     const int gi = lane / LP, li = lane % LP;
-    const u32 s = blockIdx.x * G + gi;
+    // blockIdx.x = group * slices + slice: long stripes are split into row
+    // slices on separate waves (decode rows are independent)
+    const u32 grp = blockIdx.x / u32(slices), slice = blockIdx.x % u32(slices);
+    const u32 s = grp * G + gi;
     const bool live = s < g.nstripes;
     inv4[lane] = reinterpret_cast<const u32 *>(inv)[lane];
     // the first LP offered parts and their ids, loaded in parallel
@@ -470,7 +536,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                 slot[gi][h] = sl;
                 ++h;
             }
-            if (status)
+            if (status && slice == 0)
                 status[s] = h < K ? -EINVAL : 0;
         }
         have[gi] = h;
@@ -556,50 +622,49 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
             pv[c][3] = t.w;
         }
     };
-    u32 r0 = 16 * li;
-    if (r0 < ps)
+    const u32 steps = (ps + R - 1) / R, per = (steps + slices - 1) / slices;
+    const u32 rend = min(ps, (slice + 1) * per * R);
+    u32 r0 = slice * per * R + 16 * li;
+    if (r0 < rend)
         load_step(r0);
-    for (; r0 < ps; r0 += R) {
-        u32 row[16][W];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                row[r][w] = 0;
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                const u8 *e = mytbl + c * TB + byte * E;
-                if constexpr (E == 8) {
-                    const uint2 t = *reinterpret_cast<const uint2 *>(e);
-                    row[r][0] ^= t.x;
-                    row[r][1] ^= t.y;
-                } else {
-                    row[r][0] ^= *reinterpret_cast<const u32 *>(e);
-                }
-            }
-        }
-        if (r0 + R < ps)
-            load_step(r0 + R);  // prefetch the next step under this one's stores
-        // pack 16 rows of K bytes into 4*K dwords (byte p = r*K + m)
+    for (; r0 < rend; r0 += R) {
+        // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
+        // bytes are packed into K output dwords with v_perm (<= 2 per dword)
         u32 o[4 * K];
 #pragma unroll
-        for (int q = 0; q < 4 * K; ++q) {
-            u32 x = 0;
+        for (int gq = 0; gq < 4; ++gq) {
+            u32 row[4 * W];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int p = 4 * q + b;
-                const int r = p / K, m = p % K;
-                x |= ((row[r][m >> 2] >> (8 * (m & 3))) & 0xFFu) << (8 * b);
+            for (int rr = 0; rr < 4; ++rr) {
+                const int r = 4 * gq + rr;
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    row[rr * W + w] = 0;
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                    const u8 *e = mytbl + c * TB + byte * E;
+                    if constexpr (E == 8) {
+                        const uint2 t = *reinterpret_cast<const uint2 *>(e);
+                        row[rr * W] ^= t.x;
+                        row[rr * W + 1] ^= t.y;
+                    } else {
+                        row[rr * W] ^= *reinterpret_cast<const u32 *>(e);
+                    }
+                }
             }
-            o[q] = x;
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                o[gq * K + q] = pack_dword<K, W>(row, q);
         }
+        if (r0 + R < rend)
+            load_step(r0 + R);  // prefetch the next step under this one's stores
         const u64 off = u64(r0) * K;
         if (aligned && off + 16 * K <= B) {
             uint4 *dst = reinterpret_cast<uint4 *>(out + off);
 #pragma unroll
             for (int q = 0; q < K; ++q)
-                dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                store16(dst + q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], nt);
         } else {
 #pragma unroll
             for (int q = 0; q < 4 * K; ++q)
@@ -616,22 +681,46 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
         return -ENOSYS;
-    const int G = g->k <= 4 ? 4 : 2;
-    const dim3 grid((g->nstripes + G - 1) / G);
+    // stripes per wave: E=4 tables are small, so 4 stripes share a wave;
+    // E=8 decode (k 5..8) runs one stripe per wave to halve the LDS tables
+    // and lift occupancy: C3 decode 3.27 -> 4.03 TB/s, C4 4.01 -> 4.10
+    // (tools/ab_env.py NKFS_DEC_VARIANT 0,2; variant 1 caps VGPRs at 168
+    // and spills)
     const GfTables *t = (const GfTables *)gf;
+    const bool nt = store_nt();
+    const char *ve = getenv("NKFS_DEC_VARIANT");
+    const int var = ve ? atoi(ve) : 2;
+    const int G = g->k <= 4 ? 4 : (var == 0 ? 2 : 1);
+    const u32 groups = (g->nstripes + G - 1) / G;
+    // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4 steps
+    const u32 ps = g->block_size / u32(g->k) + (g->block_size % u32(g->k) ? 1u : 0u);
+    const u32 R = 16u * (64u / u32(G));
+    const u32 steps = (ps + R - 1) / R;
+    u32 slices = 1;
+    while (groups * slices < 4096u && steps / (slices * 2) >= 4)
+        slices *= 2;
+    const dim3 grid(groups * slices);
+#define NKFS_DK(KK, EE, GG, MW)                                                                              \
+    hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, MW>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
+                       status, t->inv, nt, int(slices))
     switch (g->k) {
-#define NKFS_DK(KK, EE)                                                                                     \
-    case KK:                                                                                                \
-        hipLaunchKernelGGL((k_decode_fast<KK, EE>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
-                           status, t->inv);                                                                 \
+    case 2: NKFS_DK(2, 4, 4, 1); break;
+    case 3: NKFS_DK(3, 4, 4, 1); break;
+    case 4: NKFS_DK(4, 4, 4, 1); break;
+#define NKFS_DK8(KK)                              \
+    case KK:                                      \
+        if (var == 0)                             \
+            NKFS_DK(KK, 8, 2, 1);                 \
+        else if (var == 2)                        \
+            NKFS_DK(KK, 8, 1, 1);                 \
+        else                                      \
+            NKFS_DK(KK, 8, 1, 3);                 \
         break;
-        NKFS_DK(2, 4)
-        NKFS_DK(3, 4)
-        NKFS_DK(4, 4)
-        NKFS_DK(5, 8)
-        NKFS_DK(6, 8)
-        NKFS_DK(7, 8)
-        NKFS_DK(8, 8)
+    NKFS_DK8(5)
+    NKFS_DK8(6)
+    NKFS_DK8(7)
+    NKFS_DK8(8)
+#undef NKFS_DK8
 #undef NKFS_DK
     default:
         return -ENOSYS;

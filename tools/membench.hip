@@ -56,6 +56,84 @@ __global__ void k_read_lane_contig(const uint4 *__restrict__ a, size_t n, uint4 
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = acc;
 }
 
+// store flavours: 0 plain, 1 nontemporal (nt), 2 write-through (sc1 via
+// __hip_atomic store relaxed agent would be scalar; use inline asm)
+template <int FL>
+__device__ inline void st16(uint4 *p, uint4 v)
+{
+    if constexpr (FL == 0) {
+        *p = v;
+    } else if constexpr (FL == 1) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        v4u x = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(x) : "memory");
+    }
+}
+
+template <int FL>
+__global__ void k_r1w2_fl(const uint4 *__restrict__ a, uint4 *__restrict__ b, uint4 *__restrict__ c, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 v = a[i];
+        st16<FL>(b + i, v);
+        st16<FL>(c + i, make_uint4(v.y, v.z, v.w, v.x));
+    }
+}
+
+template <int FL>
+__global__ void k_write_fl(uint4 *__restrict__ a, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        st16<FL>(a + i, make_uint4(i, i + 1, i + 2, i + 3));
+}
+
+// the encode's write pattern: one 64-lane wave owns a REGION-byte output
+// region of STREAMS planar streams (stride REGION/STREAMS) and writes SEG
+// bytes to each stream per iteration (lanes spread evenly over streams).
+template <int STREAMS, int SEG>
+__global__ void k_wave_streams(uint4 *__restrict__ out, size_t region, size_t n_waves)
+{
+    const size_t w = blockIdx.x;
+    if (w >= n_waves) return;
+    const int lane = threadIdx.x;
+    constexpr int LPS = 64 / STREAMS;          // lanes per stream
+    constexpr int PER = SEG / 16 / LPS;        // 16-B stores per lane per stream per iteration
+    const int st = lane / LPS, li = lane % LPS;
+    const size_t stride = region / STREAMS;
+    char *base = reinterpret_cast<char *>(out) + w * region + st * stride;
+    for (size_t off = 0; off < stride; off += SEG)
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            *reinterpret_cast<uint4 *>(base + off + (size_t)(q * LPS + li) * 16) = make_uint4(off, q, li, st);
+}
+
+// encode-shaped copy: wave w reads its IN-byte input region (32 B per lane
+// per iteration, like N4K2's 16 rows x 2 B) and writes 4 parts x 4 stripes
+// (16 streams x 256 B per iteration) of its 2*IN-byte output region.
+__global__ void k_wave_r1w2(const uint4 *__restrict__ in, uint4 *__restrict__ out, size_t n_waves)
+{
+    const size_t w = blockIdx.x;
+    const int lane = threadIdx.x;
+    constexpr size_t IN = 16384;
+    const char *src = reinterpret_cast<const char *>(in) + w * IN;
+    char *dst = reinterpret_cast<char *>(out) + w * 2 * IN;
+    const int st = lane / 16, li = lane % 16;  // stripe of 4, lane in stripe
+    for (int c = 0; c < 8; ++c) {               // 8 chunks of 256 rows
+        const uint4 *p = reinterpret_cast<const uint4 *>(src + st * 4096 + c * 512 + li * 32);
+        uint4 a = p[0], b = p[1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 v = make_uint4(a.x ^ i, a.y ^ b.x, a.z ^ b.y, a.w ^ b.z + i);
+            *reinterpret_cast<uint4 *>(dst + (st * 4 + i) * 2048 + c * 256 + li * 16) = v;
+        }
+    }
+}
+
 int main()
 {
     const size_t bytes = (size_t)1 << 30;
@@ -94,6 +172,29 @@ int main()
     }
     for (int gi = 0; gi < 5; ++gi) {
         int grid = grids[gi];
+        for (int kind = 0; kind < 6; ++kind) {
+            float best = 1e9;
+            for (int rep = 0; rep < 6; ++rep) {
+                hipEventRecord(e0);
+                if (kind == 0) hipLaunchKernelGGL(k_write_fl<0>, grid, 256, 0, 0, b, n);
+                if (kind == 1) hipLaunchKernelGGL(k_write_fl<1>, grid, 256, 0, 0, b, n);
+                if (kind == 2) hipLaunchKernelGGL(k_write_fl<2>, grid, 256, 0, 0, b, n);
+                if (kind == 3) hipLaunchKernelGGL(k_r1w2_fl<0>, grid, 256, 0, 0, a, b, c, n / 2);
+                if (kind == 4) hipLaunchKernelGGL(k_r1w2_fl<1>, grid, 256, 0, 0, a, b, c, n / 2);
+                if (kind == 5) hipLaunchKernelGGL(k_r1w2_fl<2>, grid, 256, 0, 0, a, b, c, n / 2);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms;
+                hipEventElapsedTime(&ms, e0, e1);
+                if (rep && ms < best) best = ms;
+            }
+            const char *nm[] = {"write plain", "write nt", "write sc1", "r1w2 plain", "r1w2 nt", "r1w2 sc1"};
+            double moved = kind < 3 ? bytes : 1.5 * bytes;
+            printf("grid %5d  %-13s %7.1f GB/s\n", grid, nm[kind], moved / best / 1e6);
+        }
+    }
+    for (int gi = 0; gi < 5; ++gi) {
+        int grid = grids[gi];
         for (int kind = 0; kind < 3; ++kind) {
             float best = 1e9;
             for (int rep = 0; rep < 6; ++rep) {
@@ -110,6 +211,39 @@ int main()
             const char *nm[] = {"read 32B/lane", "read 80B/lane", "read 16B/lane"};
             printf("grid %5d x64  %-13s %7.1f GB/s\n", grid, nm[kind], bytes / best / 1e6);
         }
+    }
+    {
+        const size_t region = 32768, waves = bytes / region;
+        for (int kind = 0; kind < 5; ++kind) {
+            float best = 1e9;
+            for (int rep = 0; rep < 6; ++rep) {
+                hipEventRecord(e0);
+                if (kind == 0) hipLaunchKernelGGL((k_wave_streams<16, 256>), waves, 64, 0, 0, b, region, waves);
+                if (kind == 1) hipLaunchKernelGGL((k_wave_streams<16, 512>), waves, 64, 0, 0, b, region, waves);
+                if (kind == 2) hipLaunchKernelGGL((k_wave_streams<16, 1024>), waves, 64, 0, 0, b, region, waves);
+                if (kind == 3) hipLaunchKernelGGL((k_wave_streams<4, 1024>), waves, 64, 0, 0, b, region, waves);
+                if (kind == 4) hipLaunchKernelGGL((k_wave_streams<1, 1024>), waves, 64, 0, 0, b, region, waves);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms;
+                hipEventElapsedTime(&ms, e0, e1);
+                if (rep && ms < best) best = ms;
+            }
+            const char *nm[] = {"16 streams x 256B", "16 streams x 512B", "16 streams x 1KB", "4 streams x 1KB", "1 stream x 1KB"};
+            printf("wave-region write  %-18s %7.1f GB/s\n", nm[kind], bytes / best / 1e6);
+        }
+        const size_t w2 = (bytes / 2) / 16384;
+        float best = 1e9;
+        for (int rep = 0; rep < 6; ++rep) {
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k_wave_r1w2, w2, 64, 0, 0, a, b, w2);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (rep && ms < best) best = ms;
+        }
+        printf("wave-region r1w2 (encode-shaped, 16 KB in / 32 KB out per wave) %7.1f GB/s\n", 1.5 * bytes / best / 1e6);
     }
     return 0;
 }
