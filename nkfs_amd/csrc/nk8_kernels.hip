@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gf256.h"
 #include "nkfs_internal.h"
@@ -373,6 +374,9 @@ __global__ __launch_bounds__(256) void k_synth(u8 *blocks, u64 pitch, u32 B, u32
 // ----------------------------------------------------------- launchers
 
 extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, const void *gf, hipStream_t st);
+extern "C" int nkfs_fast_xxh64_list(const u8 *base, const u64 *off, const u64 *len, u32 count, u64 seed, u64 *out,
+                                    hipStream_t st);
+extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, u64 *out, hipStream_t st);
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                 int32_t *status, const void *gf, hipStream_t st);
 
@@ -422,6 +426,8 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
 
 extern "C" int nkfs_launch_hash_parts(const nkfs_geom *g, uint64_t *digests, void *stream)
 {
+    if (!getenv("NKFS_FORCE_GENERIC"))
+        return nkfs_fast_xxh64_parts(g, digests, (hipStream_t)stream);
     const u64 threads = u64(g->nstripes) * u64(g->n) * 4;
     if (!threads)
         return 0;
@@ -470,6 +476,8 @@ extern "C" int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 {
     if (!count)
         return 0;
+    if (!getenv("NKFS_FORCE_GENERIC"))
+        return nkfs_fast_xxh64_list(base, off, len, count, seed, out, (hipStream_t)stream);
     const u64 threads = u64(count) * 4;
     hipLaunchKernelGGL(k_xxh64_batch, dim3(u32((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, base,
                        off, len, count, seed, out);

@@ -282,3 +282,35 @@ def test_decode_status_too_few_distinct(L):
     st = status.cpu().tolist()
     assert st[1] == -22 and st[0] == st[2] == st[3] == 0
     assert torch.equal(out[0], blocks[0, :B]) and torch.equal(out[3], blocks[3, :B])
+
+
+def test_xxh64_batch_blocks_and_ragged(L, O):
+    """Batched XXH64 (csum seed 0) of 64 KiB blocks -- the core's per-block
+    integrity sum (core/dio.c:26-37) -- plus ragged lengths and 8-byte (not
+    16-byte) aligned offsets, against the oracle."""
+    from nkfs_amd import batch
+    rng = np.random.default_rng(9)
+    nb = 512
+    blocks = batch.synth(nb, 65536, first=99)
+    off = torch.arange(nb, dtype=torch.int64, device="cuda") * blocks.stride(0)
+    lens = torch.full((nb,), 65536, dtype=torch.int64, device="cuda")
+    got = batch.xxh64_batch(blocks, off, lens)
+    torch.cuda.synchronize()
+    host = blocks.cpu().numpy()
+    gl = [u64(x) for x in got.cpu().tolist()]
+    for i in range(0, nb, 7):
+        assert gl[i] == O.xxh64(host[i, :65536])
+    # ragged: random lengths 0..5000 at 8-byte aligned (some 16-unaligned) offsets
+    lens_np = rng.integers(0, 5000, 333)
+    offs_np = np.zeros(333, np.int64)
+    pos = 8
+    for i, n_ in enumerate(lens_np):
+        offs_np[i] = pos
+        pos += int(n_) + 8 + (8 if i % 3 else 0)
+        pos = (pos + 7) // 8 * 8
+    buf = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    got = batch.xxh64_batch(dev(buf), dev(offs_np), dev(lens_np.astype(np.int64)), seed=12345)
+    torch.cuda.synchronize()
+    gl = [u64(x) for x in got.cpu().tolist()]
+    for i in range(333):
+        assert gl[i] == O.xxh64(buf[offs_np[i]: offs_np[i] + lens_np[i]], 12345), i
