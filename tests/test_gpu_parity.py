@@ -314,3 +314,66 @@ def test_xxh64_batch_blocks_and_ragged(L, O):
     gl = [u64(x) for x in got.cpu().tolist()]
     for i in range(333):
         assert gl[i] == O.xxh64(buf[offs_np[i]: offs_np[i] + lens_np[i]], 12345), i
+
+
+@pytest.mark.parametrize("n", range(2, 9))
+def test_fast_path_every_shape(L, O, n):
+    """Every (n <= 8, k <= n) the fused kernels are instantiated for, with
+    block sizes that leave tails of every length and stripes spanning
+    several chunks, encode + XXH64 + decode from a random survivor order."""
+    from nkfs_amd import batch
+    rng = np.random.default_rng(100 + n)
+    for k in range(2, n + 1):
+        for B in (1, k - 1 or 1, k + 1, 777, 4096 * k + 3, 300_001):
+            S = 5
+            blocks = batch.synth(S, B, first=1000 * n + k)
+            ids_np = synth.batch_ids(S, n, first=1000 * n + k)
+            parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
+            torch.cuda.synchronize()
+            host = blocks.cpu().numpy()
+            ps = batch.part_size(B, k)
+            got_parts = parts.cpu().numpy()
+            got_dig = [u64(x) for x in dig.cpu().tolist()]
+            for s in range(S):
+                want = O.encode(host[s, :B], n, k, ids_np[s])
+                assert np.array_equal(got_parts[s * n:(s + 1) * n, :ps], want), (n, k, B, s)
+                assert got_dig[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], (n, k, B, s)
+            avail = np.stack([rng.permutation(n)[:k] for _ in range(S)]).astype(np.uint8)
+            out, status = batch.decode(parts, n, dev(ids_np), dev(avail), k, B)
+            torch.cuda.synchronize()
+            assert int(status.abs().sum()) == 0
+            assert torch.equal(out, blocks[:, :B]), (n, k, B)
+
+
+def test_ragged_small_n_and_unaligned(L, O):
+    """Ragged batch for n <= 4 (4 stripes per wave) with block offsets that
+    are not 16-byte aligned (the kernels' scalar load path)."""
+    from nkfs_amd import batch
+    n, k = 4, 3
+    sizes = np.array([5, 4096, 70000, 13, 65536, 1, 9999, 300], np.uint32)
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos = 3
+    ppos = 0
+    for s, B in enumerate(sizes):
+        boff[s] = pos
+        poff[s] = ppos
+        pos += int(B) + 5
+        ppos += n * batch.part_pitch(int(B), k)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff), dig,
+                        int(sizes.max()))
+    torch.cuda.synchronize()
+    got = [u64(x) for x in dig.cpu().tolist()]
+    pn = parts.cpu().numpy()
+    for s, B in enumerate(sizes):
+        want = O.encode(host[boff[s]: boff[s] + B], n, k, ids_np[s])
+        pitch = batch.part_pitch(int(B), k)
+        for i in range(n):
+            assert np.array_equal(pn[poff[s] + i * pitch: poff[s] + i * pitch + want.shape[1]], want[i]), (s, i)
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
