@@ -257,23 +257,17 @@ def cpu_baseline(S, B, n, k, target_s):
 
 
 def pcie_rate(batch, blocks_np, S, B, n, k, ids, avail, device, stream):
-    """Host-memory path: pinned H2D of the blocks, encode+decode, D2H of the
-    parts and the digests (DESIGN.md records it; never the headline)."""
+    """Host-memory path (nkfs_nk8_encode_host): pinned host blocks -> H2D ->
+    fused encode+XXH64 -> D2H of parts and digests, sub-batches pipelined
+    on two streams.  User GiB/s; DESIGN.md records it (never the headline)."""
     import torch
     host_in = torch.from_numpy(blocks_np).pin_memory()
-    ps = batch.part_pitch(B, k)
-    host_parts = torch.empty((S * n, ps), dtype=torch.uint8).pin_memory()
-    dev_in = torch.empty((S, B), dtype=torch.uint8, device=device)
-    parts = torch.empty((S * n, ps), dtype=torch.uint8, device=device)
-    dig = torch.empty(S * n, dtype=torch.int64, device=device)
-    torch.cuda.synchronize(device)
-    reps = 5
+    ids_h = ids.cpu()
+    batch.encode_host(host_in, B, n, k, ids_h)  # warm-up (allocations, pinning)
+    reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        dev_in.copy_(host_in, non_blocking=True)
-        batch.encode(dev_in, B, n, k, ids, parts, dig, stream=stream)
-        host_parts.copy_(parts, non_blocking=True)
-    torch.cuda.synchronize(device)
+        parts, dig = batch.encode_host(host_in, B, n, k, ids_h)
     t1 = time.perf_counter()
     return round(S * B * reps / (t1 - t0) / 2**30, 3)
 

@@ -81,6 +81,20 @@ int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off,
 		     const uint64_t *d_len, uint32_t count, uint64_t seed,
 		     uint64_t *d_out, void *stream);
 
+/* Host-memory form of nkfs_nk8_encode: blocks, ids, parts and digests in
+ * host memory (the path's real entry: socket -> page buffers -> device,
+ * SURVEY.md §8(f) row 2).  The batch is cut into sub-batches of about
+ * `chunk_bytes` of user data that flow through two streams, so the H2D of
+ * one sub-batch, the fused encode+XXH64 of the previous and the D2H of its
+ * parts overlap.  Host buffers that are not already pinned are registered
+ * (hipHostRegister) for the duration of the call.  Synchronous: returns
+ * when parts and digests are in host memory.  chunk_bytes 0 = 32 MiB. */
+int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch,
+			 uint32_t block_size, uint32_t nstripes, int n, int k,
+			 const uint8_t *h_ids, uint8_t *h_parts,
+			 uint64_t part_pitch, uint64_t *h_digests,
+			 uint64_t chunk_bytes);
+
 /* Fill a uniform batch with the seeded counter-based splitmix64 stripes of
  * nkfs_amd/synth.py (bench / test input synthesis on the device). */
 int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch,

@@ -104,6 +104,25 @@ def decode(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Te
     return out, status
 
 
+def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int = 0, digests: bool = True):
+    """Host-memory encode (+XXH64): blocks uint8 [nstripes, pitch] and ids
+    uint8 [nstripes, n] as numpy arrays or CPU tensors (pinned is fastest);
+    streams through the GPU in sub-batches (nkfs_nk8_encode_host).
+    Returns (parts [nstripes*n, part_pitch] CPU tensor, digests or None)."""
+    bt = torch.as_tensor(blocks)
+    it = torch.as_tensor(ids)
+    if bt.dtype != U8 or it.dtype != U8 or bt.is_cuda or it.is_cuda or not bt.is_contiguous():
+        raise ValueError("blocks/ids: contiguous uint8 host arrays")
+    nstripes = bt.shape[0]
+    pitch = part_pitch(block_size, k)
+    parts = torch.empty((nstripes * n, pitch), dtype=U8, pin_memory=torch.cuda.is_available())
+    dig = torch.empty(nstripes * n, dtype=torch.int64, pin_memory=torch.cuda.is_available()) if digests else None
+    check(lib().nkfs_nk8_encode_host(bt.data_ptr(), bt.stride(0) if bt.dim() > 1 else block_size, block_size,
+                                     nstripes, n, k, it.contiguous().data_ptr(), parts.data_ptr(), pitch,
+                                     _ptr(dig), chunk_bytes), "nkfs_nk8_encode_host")
+    return parts, dig
+
+
 def xxh64_batch(base: torch.Tensor, off: torch.Tensor, lens: torch.Tensor, seed: int = 0, stream=None):
     _need(base, U8, "base")
     out = torch.empty(off.numel(), dtype=torch.int64, device=base.device)

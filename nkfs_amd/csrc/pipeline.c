@@ -1,0 +1,133 @@
+/*
+ * pipeline.c -- host-memory entry points: sub-batches streamed through the
+ * GPU on two streams so that PCIe H2D, the fused kernels and PCIe D2H
+ * overlap (the reference's path starts and ends in host memory: client
+ * socket -> core/upages.c page buffers -> block device).
+ */
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "../../include/nkfs_gpu.h"
+#include "nkfs_internal.h"
+#include "runtime.h"
+
+/* pin a caller buffer for the call unless the runtime already knows it */
+static int pin(const void *p, size_t bytes, int *registered)
+{
+	*registered = 0;
+	if (!p || !bytes)
+		return 0;
+	hipPointerAttribute_t attr;
+	if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost)
+		return 0;
+	(void)hipGetLastError();
+	hipError_t e = hipHostRegister((void *)p, bytes, hipHostRegisterDefault);
+	if (e == hipErrorHostMemoryAlreadyRegistered) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	if (e != hipSuccess)
+		return nkfs_hip_fail("hipHostRegister", (int)e);
+	*registered = 1;
+	return 0;
+}
+
+#define NSTREAM 2
+
+int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
+			 int n, int k, const uint8_t *h_ids, uint8_t *h_parts, uint64_t part_pitch,
+			 uint64_t *h_digests, uint64_t chunk_bytes)
+{
+	if (nkfs_bad_params(block_size, n, k))
+		return -EINVAL;
+	if (!nkfs_gpu_ready())
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!h_blocks || !h_ids || !h_parts || part_pitch < nkfs_part_size(block_size, k) || (part_pitch & 15) ||
+	    (nstripes > 1 && block_pitch < block_size))
+		return -EINVAL;
+	if (!chunk_bytes)
+		chunk_bytes = 32ull << 20;
+	uint32_t per = (uint32_t)(chunk_bytes / block_size);
+	if (per < 1)
+		per = 1;
+	if (per > nstripes)
+		per = nstripes;
+
+	const uint64_t bp = block_pitch ? block_pitch : block_size;
+	const uint64_t in_bytes = (uint64_t)(nstripes - 1) * bp + block_size;
+	const uint64_t parts_bytes = (uint64_t)nstripes * n * part_pitch;
+	int reg[4] = {0, 0, 0, 0}, err;
+	if ((err = pin(h_blocks, in_bytes, &reg[0])) || (err = pin(h_ids, (size_t)nstripes * n, &reg[1])) ||
+	    (err = pin(h_parts, parts_bytes, &reg[2])) ||
+	    (err = pin(h_digests, h_digests ? (size_t)nstripes * n * 8 : 0, &reg[3])))
+		goto unpin;
+
+	/* per stream: blocks | parts | ids | digests (device) */
+	const uint64_t dblk = (uint64_t)per * bp;
+	const uint64_t dparts = (uint64_t)per * n * part_pitch;
+	const uint64_t dids = ((uint64_t)per * n + 255) & ~255ull;
+	const uint64_t ddig = (uint64_t)per * n * 8;
+	const uint64_t slot = ((dblk + 255) & ~255ull) + dparts + dids + ddig;
+	hipStream_t st[NSTREAM] = {0};
+	uint8_t *dev = NULL;
+	hipError_t e = hipMalloc((void **)&dev, slot * NSTREAM);
+	for (int i = 0; e == hipSuccess && i < NSTREAM; i++)
+		e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+	if (e != hipSuccess) {
+		err = nkfs_hip_fail("pipeline setup", (int)e);
+		goto out;
+	}
+	for (uint32_t s0 = 0, it = 0; s0 < nstripes; s0 += per, it++) {
+		const uint32_t cnt = nstripes - s0 < per ? nstripes - s0 : per;
+		hipStream_t s = st[it % NSTREAM];
+		uint8_t *d = dev + slot * (it % NSTREAM);
+		uint8_t *d_blk = d, *d_parts = d + ((dblk + 255) & ~255ull);
+		uint8_t *d_ids = d_parts + dparts;
+		uint64_t *d_dig = (uint64_t *)(d_ids + dids);
+		const uint64_t nin = (uint64_t)(cnt - 1) * bp + block_size;
+		if ((e = hipMemcpyAsync(d_blk, h_blocks + (uint64_t)s0 * bp, nin, hipMemcpyHostToDevice, s)) ||
+		    (e = hipMemcpyAsync(d_ids, h_ids + (uint64_t)s0 * n, (size_t)cnt * n, hipMemcpyHostToDevice, s))) {
+			err = nkfs_hip_fail("H2D", (int)e);
+			goto out;
+		}
+		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k };
+		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), s)))
+			goto out;
+		if ((e = hipMemcpyAsync(h_parts + (uint64_t)s0 * n * part_pitch, d_parts, (uint64_t)cnt * n * part_pitch,
+					hipMemcpyDeviceToHost, s)) ||
+		    (h_digests && (e = hipMemcpyAsync(h_digests + (uint64_t)s0 * n, d_dig, (size_t)cnt * n * 8,
+						       hipMemcpyDeviceToHost, s)))) {
+			err = nkfs_hip_fail("D2H", (int)e);
+			goto out;
+		}
+	}
+	for (int i = 0; i < NSTREAM; i++)
+		if ((e = hipStreamSynchronize(st[i])) != hipSuccess) {
+			err = nkfs_hip_fail("pipeline sync", (int)e);
+			goto out;
+		}
+	err = 0;
+out:
+	for (int i = 0; i < NSTREAM; i++)
+		if (st[i]) {
+			hipStreamSynchronize(st[i]);
+			hipStreamDestroy(st[i]);
+		}
+	hipFree(dev);
+unpin:
+	if (reg[0])
+		hipHostUnregister((void *)h_blocks);
+	if (reg[1])
+		hipHostUnregister((void *)h_ids);
+	if (reg[2])
+		hipHostUnregister(h_parts);
+	if (reg[3])
+		hipHostUnregister(h_digests);
+	return err;
+}

@@ -377,3 +377,22 @@ def test_ragged_small_n_and_unaligned(L, O):
         for i in range(n):
             assert np.array_equal(pn[poff[s] + i * pitch: poff[s] + i * pitch + want.shape[1]], want[i]), (s, i)
         assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
+
+
+def test_encode_host_pipeline(L, O):
+    """nkfs_nk8_encode_host (host memory in/out, sub-batches overlapped on
+    two streams) equals the device-resident encode, for pageable numpy
+    input (registered for the call) and several sub-batch sizes."""
+    from nkfs_amd import batch
+    S, B, n, k = 3000, 4096, 4, 2
+    blocks = batch.synth(S, B)
+    ids_np = synth.batch_ids(S, n)
+    parts_d, dig_d = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    host = np.ascontiguousarray(blocks.cpu().numpy())
+    for chunk in (0, 1 << 20, 123457):
+        parts_h, dig_h = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=chunk)
+        assert torch.equal(parts_h[:, :2048], parts_d[:, :2048].cpu())
+        assert torch.equal(dig_h, dig_d.cpu())
+    blk = host[17, :B]
+    assert [O.xxh64(p) for p in O.encode(blk, n, k, ids_np[17])] == [u64(x) for x in dig_h[17 * n:18 * n].tolist()]
