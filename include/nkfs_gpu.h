@@ -74,6 +74,22 @@ int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots,
 		    uint64_t block_pitch, uint32_t nstripes, void *d_work,
 		    int32_t *d_status, void *stream);
 
+/* nkfs_nk8_decode that also verifies every part it reads against its stored
+ * digest (d_expect[s*n_slots + j] = XXH64 of slot j, as produced by
+ * nkfs_nk8_encode), the GET-side check of the core's per-block sums
+ * (core/inode.c:561-575).  The check is fused into the rebuild (no second
+ * pass over the parts).  A stripe with a mismatching part gets status -EIO
+ * and d_badmask[s] (may be NULL) bit j set for each failing slot j < 63
+ * (bit 63 for slots >= 63); the rebuilt block is still written. */
+int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch,
+			   int n_slots, const uint8_t *d_ids,
+			   const uint8_t *d_avail, int navail, int k,
+			   uint32_t block_size, uint8_t *d_blocks,
+			   uint64_t block_pitch, uint32_t nstripes,
+			   void *d_work, int32_t *d_status,
+			   const uint64_t *d_expect, uint64_t *d_badmask,
+			   void *stream);
+
 /* XXH64 of `count` messages d_base + d_off[i], d_len[i] bytes each
  * (d_off[i] a multiple of 8) -- the batched form of csum_* for the core's
  * per-64 KiB-block integrity sums (core/dio.c:26-37). */

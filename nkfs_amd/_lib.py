@@ -54,6 +54,8 @@ _SIGS = {
     "nkfs_decode_workspace": (C.c_uint64, [C.c_uint32, C.c_int]),
     "nkfs_nk8_decode": (C.c_int, [vp, C.c_uint64, C.c_int, vp, vp, C.c_int, C.c_int, C.c_uint32, vp, C.c_uint64,
                                   C.c_uint32, vp, vp, vp]),
+    "nkfs_nk8_decode_verify": (C.c_int, [vp, C.c_uint64, C.c_int, vp, vp, C.c_int, C.c_int, C.c_uint32, vp,
+                                         C.c_uint64, C.c_uint32, vp, vp, vp, vp, vp]),
     "nkfs_xxh64_batch": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint64, vp, vp]),
     "nkfs_nk8_encode_host": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int, vp, vp,
                                        C.c_uint64, vp, C.c_uint64]),

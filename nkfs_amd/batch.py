@@ -104,6 +104,33 @@ def decode(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Te
     return out, status
 
 
+def decode_verify(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Tensor, k: int,
+                  block_size: int, expect: torch.Tensor, out: torch.Tensor | None = None,
+                  work: torch.Tensor | None = None, status: torch.Tensor | None = None, stream=None):
+    """decode() that also checks each part it reads against expect
+    [nstripes * n_slots] (int64 XXH64 digests).  Returns (blocks, status,
+    badmask): status -EIO and badmask bit j for a mismatching slot j."""
+    _need(parts, U8, "parts")
+    _need(ids, U8, "ids")
+    _need(avail, U8, "avail")
+    _need(expect, torch.int64, "expect")
+    nstripes, navail = avail.shape[0], avail.shape[1]
+    dev = parts.device
+    if out is None:
+        out = torch.empty((nstripes, block_size), dtype=U8, device=dev)
+    if work is None:
+        work = decode_workspace(nstripes, k, dev)
+    if status is None:
+        status = torch.empty(nstripes, dtype=torch.int32, device=dev)
+    bad = torch.empty(nstripes, dtype=torch.int64, device=dev)
+    check(lib().nkfs_nk8_decode_verify(parts.data_ptr(), parts.stride(0), n_slots, ids.data_ptr(),
+                                       avail.data_ptr(), navail, k, block_size, out.data_ptr(),
+                                       out.stride(0) if out.dim() > 1 else block_size, nstripes, work.data_ptr(),
+                                       status.data_ptr(), expect.data_ptr(), bad.data_ptr(), _stream(stream)),
+          "nkfs_nk8_decode_verify")
+    return out, status, bad
+
+
 def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int = 0, digests: bool = True):
     """Host-memory encode (+XXH64): blocks uint8 [nstripes, pitch] and ids
     uint8 [nstripes, n] as numpy arrays or CPU tensors (pinned is fastest);

@@ -197,7 +197,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 	struct nkfs_geom g = { d + off_block, round16(block_size), block_size, NULL, NULL, d + off_parts, pitch,
 			       NULL, 1, k, k };
 	if ((err = nkfs_launch_decode(&g, k, d + off_ids, d + off_avail, k, d + off_work,
-				      (int32_t *)(d + off_status), nkfs_gf(), c->stream)))
+				      (int32_t *)(d + off_status), nkfs_gf(), c->stream, NULL, NULL)))
 		goto out;
 	HIPGO(hipMemcpyAsync(block, d + off_block, block_size, hipMemcpyDeviceToHost, c->stream));
 	int32_t st = 0;

@@ -482,16 +482,19 @@ __device__ inline u32 gfm(u32 a, u32 b)
 
 }  // namespace
 
-template <int K, int E, int G, int MINW>
-__global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                          int navail, int32_t *status, const u8 *inv, bool nt,
-                                                          int slices)
+template <int K, int E, int G, bool VERIFY>
+__global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
+                                                    int navail, int32_t *status, const u8 *inv, bool nt, int slices,
+                                                    const u64 *expect, u64 *badmask)
 {
     constexpr int LP = 64 / G;
     constexpr int R = 16 * LP;  // rows per stripe per step
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
+    constexpr int SPX = R + 32;  // verify exchange buffer bytes per part
+    static_assert(!VERIFY || 4 * K <= LP, "one hash chain per lane");
     __shared__ __attribute__((aligned(16))) u8 tbl[G * K * TB];
+    __shared__ __attribute__((aligned(16))) u8 xbuf[VERIFY ? G * K * SPX : 16];
     __shared__ u8 slot[G][K], M[G][K + 1], xs[G][K], wrow[G][K][K];
     __shared__ u8 cand_id[G][LP], cand_slot[G][LP];
     __shared__ u32 inv4[64];  // GF inverses, 4 per word
@@ -538,6 +541,8 @@ __global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slo
             }
             if (status && slice == 0)
                 status[s] = h < K ? -EINVAL : 0;
+            if (VERIFY && badmask)
+                badmask[s] = 0;
         }
         have[gi] = h;
         if (h == K) {
@@ -622,15 +627,9 @@ __global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slo
             pv[c][3] = t.w;
         }
     };
-    const u32 steps = (ps + R - 1) / R, per = (steps + slices - 1) / slices;
-    const u32 rend = min(ps, (slice + 1) * per * R);
-    u32 r0 = slice * per * R + 16 * li;
-    if (r0 < rend)
-        load_step(r0);
-    for (; r0 < rend; r0 += R) {
+    auto rebuild = [&](u32 (&o)[4 * K]) {
         // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
         // bytes are packed into K output dwords with v_perm (<= 2 per dword)
-        u32 o[4 * K];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             u32 row[4 * W];
@@ -657,8 +656,8 @@ __global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slo
             for (int q = 0; q < K; ++q)
                 o[gq * K + q] = pack_dword<K, W>(row, q);
         }
-        if (r0 + R < rend)
-            load_step(r0 + R);  // prefetch the next step under this one's stores
+    };
+    auto emit = [&](const u32 (&o)[4 * K], u32 r0) {
         const u64 off = u64(r0) * K;
         if (aligned && off + 16 * K <= B) {
             uint4 *dst = reinterpret_cast<uint4 *>(out + off);
@@ -672,11 +671,98 @@ __global__ __launch_bounds__(64, MINW) void k_decode_fast(nkfs_geom g, int n_slo
                     if (off + 4 * q + b < B)
                         out[off + 4 * q + b] = u8(o[q] >> (8 * b));
         }
+    };
+
+    if constexpr (!VERIFY) {
+        const u32 steps = (ps + R - 1) / R, per = (steps + slices - 1) / slices;
+        const u32 rend = min(ps, (slice + 1) * per * R);
+        u32 r0 = slice * per * R + 16 * li;
+        if (r0 < rend)
+            load_step(r0);
+        for (; r0 < rend; r0 += R) {
+            u32 o[4 * K];
+            rebuild(o);
+            if (r0 + R < rend)
+                load_step(r0 + R);  // prefetch the next step under this one's stores
+            emit(o, r0);
+        }
+    } else {
+        // Integrity-checked decode: the k parts read for the rebuild are also
+        // hashed (XXH64, seed 0) and compared with their stored digests, as
+        // the core checks every block it reads (core/inode.c:561-575).  One
+        // lane per (part, accumulator); words reach the hash lanes through
+        // LDS and the rounds of step t-1 run beside the lookups of step t.
+        constexpr int RPC = R / 32;
+        const int hc = li >> 2, ha = li & 3;
+        const bool hlane = li < 4 * K;
+        const u32 nst = ps >> 5;
+        const u32 steps = (ps + R - 1) / R;
+        u64 acc = xxh_acc_init(ha, 0);
+        u64 hw[RPC];
+        int hvalid = 0;
+        if (16 * li < ps)
+            load_step(16 * li);
+        for (u32 t = 0; t <= steps; ++t) {
+            const u32 r0 = t * R + 16 * li;
+            const bool act = t < steps && r0 < ps;
+            u32 o[4 * K];
+            if (act)
+                rebuild(o);
+#pragma unroll
+            for (int r = 0; r < RPC; ++r) {
+                const u64 nxt = xxh_round(acc, hw[r]);
+                acc = r < hvalid ? nxt : acc;
+            }
+            if (act) {
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    *reinterpret_cast<uint4 *>(xbuf + (gi * K + c) * SPX + 16 * li) =
+                        make_uint4(pv[c][0], pv[c][1], pv[c][2], pv[c][3]);
+                if (r0 + R < ps)
+                    load_step(r0 + R);
+                emit(o, r0);
+            }
+            __syncthreads();
+            hvalid = 0;
+            if (hlane && t < steps) {
+                const u8 *hsrc = xbuf + (gi * K + hc) * SPX + 8 * ha;
+                const int left = int(nst) - int(t * RPC);
+                hvalid = left < 0 ? 0 : (left > RPC ? RPC : left);
+#pragma unroll
+                for (int r = 0; r < RPC; ++r)
+                    hw[r] = *reinterpret_cast<const u64 *>(hsrc + 32 * r);
+            }
+            __syncthreads();
+        }
+        const int base = lane & ~3;
+        const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+        const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+        if (hlane && ha == 0) {
+            u64 h = ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+            h += ps;
+            u64 tw[4] = {0, 0, 0, 0};
+            const u32 left = ps & 31;
+            if (left) {
+                const u32 toff = nst * 32 - (steps - 1) * R;
+                const u64 *tp = reinterpret_cast<const u64 *>(xbuf + (gi * K + hc) * SPX + toff);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    tw[w] = tp[w];
+            }
+            const u8 sl = slot[gi][hc];
+            if (xxh_tail_regs(h, tw, left) != expect[u64(s) * n_slots + sl]) {
+                if (badmask)
+                    atomicOr(reinterpret_cast<unsigned long long *>(badmask + s), 1ull << (sl < 63 ? sl : 63));
+                if (status)
+                    status[s] = -EIO;
+            }
+        }
     }
 }
 
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *gf, hipStream_t st)
+                                int navail, int32_t *status, const void *gf, hipStream_t st,
+                                const uint64_t *expect, uint64_t *badmask)
 {
     if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
@@ -684,43 +770,38 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     // stripes per wave: E=4 tables are small, so 4 stripes share a wave;
     // E=8 decode (k 5..8) runs one stripe per wave to halve the LDS tables
     // and lift occupancy: C3 decode 3.27 -> 4.03 TB/s, C4 4.01 -> 4.10
-    // (tools/ab_env.py NKFS_DEC_VARIANT 0,2; variant 1 caps VGPRs at 168
-    // and spills)
+    // (tools/ab_env.py, 2 vs 1 stripe per wave).
     const GfTables *t = (const GfTables *)gf;
     const bool nt = store_nt();
-    const char *ve = getenv("NKFS_DEC_VARIANT");
-    const int var = ve ? atoi(ve) : 2;
-    const int G = g->k <= 4 ? 4 : (var == 0 ? 2 : 1);
+    const bool verify = expect != nullptr;
+    const int G = g->k <= 4 ? 4 : 1;
     const u32 groups = (g->nstripes + G - 1) / G;
-    // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4 steps
+    // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4
+    // steps; the verifying form hashes each part in order: one slice
     const u32 ps = g->block_size / u32(g->k) + (g->block_size % u32(g->k) ? 1u : 0u);
     const u32 R = 16u * (64u / u32(G));
     const u32 steps = (ps + R - 1) / R;
     u32 slices = 1;
-    while (groups * slices < 4096u && steps / (slices * 2) >= 4)
+    while (!verify && groups * slices < 4096u && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
-#define NKFS_DK(KK, EE, GG, MW)                                                                              \
-    hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, MW>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, navail, \
-                       status, t->inv, nt, int(slices))
+#define NKFS_DK(KK, EE, GG)                                                                                     \
+    do {                                                                                                        \
+        if (verify)                                                                                             \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, true>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, \
+                               navail, status, t->inv, nt, int(slices), expect, badmask);                       \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, false>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
+                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
+    } while (0)
     switch (g->k) {
-    case 2: NKFS_DK(2, 4, 4, 1); break;
-    case 3: NKFS_DK(3, 4, 4, 1); break;
-    case 4: NKFS_DK(4, 4, 4, 1); break;
-#define NKFS_DK8(KK)                              \
-    case KK:                                      \
-        if (var == 0)                             \
-            NKFS_DK(KK, 8, 2, 1);                 \
-        else if (var == 2)                        \
-            NKFS_DK(KK, 8, 1, 1);                 \
-        else                                      \
-            NKFS_DK(KK, 8, 1, 3);                 \
-        break;
-    NKFS_DK8(5)
-    NKFS_DK8(6)
-    NKFS_DK8(7)
-    NKFS_DK8(8)
-#undef NKFS_DK8
+    case 2: NKFS_DK(2, 4, 4); break;
+    case 3: NKFS_DK(3, 4, 4); break;
+    case 4: NKFS_DK(4, 4, 4); break;
+    case 5: NKFS_DK(5, 8, 1); break;
+    case 6: NKFS_DK(6, 8, 1); break;
+    case 7: NKFS_DK(7, 8, 1); break;
+    case 8: NKFS_DK(8, 8, 1); break;
 #undef NKFS_DK
     default:
         return -ENOSYS;

@@ -343,6 +343,47 @@ __global__ __launch_bounds__(256) void k_decode_generic(nkfs_geom g, int n_slots
     }
 }
 
+// Integrity check for the general decode path: XXH64 of the k parts the
+// prep kernel selected, compared with their stored digests; a mismatch sets
+// status -EIO and the slot's bit in badmask (bit 63 for slots >= 63).
+__global__ __launch_bounds__(64) void k_verify_generic(nkfs_geom g, int n_slots, const u8 *work, int32_t *status,
+                                                       const u64 *expect, u64 *badmask)
+{
+    const u32 s = blockIdx.x;
+    const int k = g.k;
+    if (status && status[s] == -EINVAL)
+        return;
+    const u8 *wk = work + u64(s) * u64(k + k * k);
+    const u32 ps = part_size_of(g.block_size, k);
+    const u32 nst = ps >> 5;
+    if (threadIdx.x == 0 && badmask)
+        badmask[s] = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < k; c0 += 16) {
+        const int c = c0 + int(threadIdx.x >> 2), a = int(threadIdx.x & 3);
+        const bool live = c < k;
+        const u8 sl = live ? wk[c] : 0;
+        const u8 *p = g.parts + (u64(s) * n_slots + sl) * g.part_pitch;
+        u64 acc = xxh_acc_init(a, 0);
+        const u64 *w = reinterpret_cast<const u64 *>(p) + a;
+        for (u32 r = 0; live && r < nst; ++r)
+            acc = xxh_round(acc, w[4 * r]);
+        const int b = int(threadIdx.x & 63) & ~3;
+        const u64 v1 = shfl64(acc, b), v2 = shfl64(acc, b + 1);
+        const u64 v3 = shfl64(acc, b + 2), v4 = shfl64(acc, b + 3);
+        if (live && a == 0) {
+            u64 h = ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+            h += ps;
+            if (xxh_tail(h, p + (u64(nst) << 5), ps & 31) != expect[u64(s) * n_slots + sl]) {
+                if (badmask)
+                    atomicOr(reinterpret_cast<unsigned long long *>(badmask + s), 1ull << (sl < 63 ? sl : 63));
+                if (status)
+                    status[s] = -EIO;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------- synthetic
 // word(seed, s, w) = mix64(seed + GAMMA*((s << 32) + w + 1)) -- synth.py.
 __device__ inline u64 mix64(u64 z)
@@ -378,7 +419,7 @@ extern "C" int nkfs_fast_xxh64_list(const u8 *base, const u64 *off, const u64 *l
                                     hipStream_t st);
 extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, u64 *out, hipStream_t st);
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
-                                int32_t *status, const void *gf, hipStream_t st);
+                                int32_t *status, const void *gf, hipStream_t st, const u64 *expect, u64 *badmask);
 
 static int launch_ok(void)
 {
@@ -437,12 +478,13 @@ extern "C" int nkfs_launch_hash_parts(const nkfs_geom *g, uint64_t *digests, voi
 }
 
 extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                  int navail, void *work, int32_t *status, const void *gf, void *stream)
+                                  int navail, void *work, int32_t *status, const void *gf, void *stream,
+                                  const uint64_t *expect, uint64_t *badmask)
 {
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
-    int rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st);
+    int rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
     if (rc != -ENOSYS)
         return rc;
     hipLaunchKernelGGL(k_decode_prep, dim3(g->nstripes), dim3(64), 0, st, ids, avail, n_slots, navail, g->k,
@@ -454,6 +496,10 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     dim3 grid(g->nstripes, (ps + 255) / 256);
     hipLaunchKernelGGL(k_decode_generic, grid, dim3(256), 0, st, *g, n_slots, (const u8 *)work,
                        (const int32_t *)status, (const GfTables *)gf);
+    if ((rc = launch_ok()) || !expect)
+        return rc;
+    hipLaunchKernelGGL(k_verify_generic, dim3(g->nstripes), dim3(64), 0, st, *g, n_slots, (const u8 *)work, status,
+                       expect, badmask);
     return launch_ok();
 }
 

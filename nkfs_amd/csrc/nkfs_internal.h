@@ -37,7 +37,7 @@ int nkfs_launch_hash_parts(const struct nkfs_geom *g, uint64_t *digests,
 int nkfs_launch_decode(const struct nkfs_geom *g, int n_slots,
 		       const uint8_t *ids, const uint8_t *avail, int navail,
 		       void *work, int32_t *status, const void *gf_tables,
-		       void *stream);
+		       void *stream, const uint64_t *expect, uint64_t *badmask);
 int nkfs_launch_xxh64_stripes(uint64_t *state_v, const uint8_t *data,
 			      uint64_t nstripes32, void *stream);
 int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v,

@@ -256,9 +256,10 @@ uint64_t nkfs_decode_workspace(uint32_t nstripes, int k)
 	return nkfs_decode_work_bytes(nstripes, k);
 }
 
-int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
-		    const uint8_t *d_avail, int navail, int k, uint32_t block_size, uint8_t *d_blocks,
-		    uint64_t block_pitch, uint32_t nstripes, void *d_work, int32_t *d_status, void *stream)
+static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
+			 const uint8_t *d_avail, int navail, int k, uint32_t block_size, uint8_t *d_blocks,
+			 uint64_t block_pitch, uint32_t nstripes, void *d_work, int32_t *d_status,
+			 const uint64_t *d_expect, uint64_t *d_badmask, void *stream)
 {
 	if (nkfs_bad_params(block_size, navail, k) || n_slots < 1 || n_slots > 255)
 		return -EINVAL;
@@ -271,7 +272,27 @@ int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, co
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
 			       nstripes, n_slots, k };
-	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream);
+	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, d_expect,
+				  d_badmask);
+}
+
+int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
+		    const uint8_t *d_avail, int navail, int k, uint32_t block_size, uint8_t *d_blocks,
+		    uint64_t block_pitch, uint32_t nstripes, void *d_work, int32_t *d_status, void *stream)
+{
+	return decode_common(d_parts, part_pitch, n_slots, d_ids, d_avail, navail, k, block_size, d_blocks,
+			     block_pitch, nstripes, d_work, d_status, NULL, NULL, stream);
+}
+
+int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
+			   const uint8_t *d_avail, int navail, int k, uint32_t block_size, uint8_t *d_blocks,
+			   uint64_t block_pitch, uint32_t nstripes, void *d_work, int32_t *d_status,
+			   const uint64_t *d_expect, uint64_t *d_badmask, void *stream)
+{
+	if (!d_expect)
+		return -EINVAL;
+	return decode_common(d_parts, part_pitch, n_slots, d_ids, d_avail, navail, k, block_size, d_blocks,
+			     block_pitch, nstripes, d_work, d_status, d_expect, d_badmask, stream);
 }
 
 int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off, const uint64_t *d_len, uint32_t count,

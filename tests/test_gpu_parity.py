@@ -396,3 +396,38 @@ def test_encode_host_pipeline(L, O):
         assert torch.equal(dig_h, dig_d.cpu())
     blk = host[17, :B]
     assert [O.xxh64(p) for p in O.encode(blk, n, k, ids_np[17])] == [u64(x) for x in dig_h[17 * n:18 * n].tolist()]
+
+
+@pytest.mark.parametrize("S,B,n,k", [(64, 4096, 4, 2), (16, 262144, 8, 5), (40, 70001, 6, 3), (8, 30000, 16, 12),
+                                     (33, 100, 8, 8)])
+def test_decode_verify(L, S, B, n, k):
+    """Integrity-checked decode: clean parts verify; a flipped byte in a
+    part that is read fails its stripe with -EIO and flags exactly that slot;
+    a flipped byte in a part that is not read changes nothing."""
+    from nkfs_amd import batch
+    rng = np.random.default_rng(S + B)
+    blocks = batch.synth(S, B, first=5)
+    ids_np = synth.batch_ids(S, n, first=5)
+    ids = dev(ids_np)
+    parts, dig = batch.encode(blocks, B, n, k, ids)
+    avail_np = np.stack([rng.permutation(n)[:k] for _ in range(S)]).astype(np.uint8)
+    avail = dev(avail_np)
+    out, status, bad = batch.decode_verify(parts, n, ids, avail, k, B, dig)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0 and int(bad.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])
+    ps = batch.part_size(B, k)
+    s_used, s_unused = 1, 2
+    used_slot = int(avail_np[s_used, 1])
+    unused = [j for j in range(n) if j not in avail_np[s_unused]]
+    parts[s_used * n + used_slot, ps - 1] ^= 0x5A
+    if unused:
+        parts[s_unused * n + unused[0], 0] ^= 0xA5
+    out, status, bad = batch.decode_verify(parts, n, ids, avail, k, B, dig)
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    bm = [u64(x) for x in bad.cpu().tolist()]
+    assert st[s_used] == -5 and bm[s_used] == 1 << used_slot
+    assert st[s_unused] == 0 and bm[s_unused] == 0
+    assert all(v == 0 for i, v in enumerate(st) if i != s_used)
+    assert torch.equal(out[s_unused], blocks[s_unused, :B])

@@ -134,6 +134,36 @@ __global__ void k_wave_r1w2(const uint4 *__restrict__ in, uint4 *__restrict__ ou
     }
 }
 
+// encode-shaped copy variants.  SPW stripes per wave (4 KiB in, 4 x 2 KiB
+// out each), ROWS16 16-row tasks per lane per chunk.
+template <int SPW, int T16>
+__global__ void k_enc_shape(const uint4 *__restrict__ in, uint4 *__restrict__ out, size_t n_waves)
+{
+    const size_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (w >= n_waves) return;
+    const int lane = threadIdx.x & 63;
+    constexpr int LPS = 64 / SPW;                  // lanes per stripe
+    constexpr int R = 16 * T16 * LPS;              // rows per chunk per stripe
+    const int st = lane / LPS, li = lane % LPS;
+    const char *src = reinterpret_cast<const char *>(in) + (w * SPW + st) * 4096;
+    char *dst = reinterpret_cast<char *>(out) + (w * SPW + st) * 8192;
+    for (int c = 0; c < 2048 / R; ++c) {
+        uint4 a[2 * T16];
+#pragma unroll
+        for (int t = 0; t < T16; ++t) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(src + (c * R + (t * LPS + li) * 16) * 2);
+            a[2 * t] = p[0];
+            a[2 * t + 1] = p[1];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int t = 0; t < T16; ++t)
+                *reinterpret_cast<uint4 *>(dst + i * 2048 + c * R + (t * LPS + li) * 16) =
+                    make_uint4(a[2 * t].x ^ i, a[2 * t].y, a[2 * t + 1].z, a[2 * t + 1].w + i);
+    }
+}
+
 int main()
 {
     const size_t bytes = (size_t)1 << 30;
@@ -244,6 +274,27 @@ int main()
             if (rep && ms < best) best = ms;
         }
         printf("wave-region r1w2 (encode-shaped, 16 KB in / 32 KB out per wave) %7.1f GB/s\n", 1.5 * bytes / best / 1e6);
+        const size_t stripes = (bytes / 2) / 4096;
+        for (int kind = 0; kind < 6; ++kind) {
+            float bb = 1e9;
+            for (int rep = 0; rep < 6; ++rep) {
+                hipEventRecord(e0);
+                if (kind == 0) hipLaunchKernelGGL((k_enc_shape<4, 1>), stripes / 4, 64, 0, 0, a, b, stripes / 4);
+                if (kind == 1) hipLaunchKernelGGL((k_enc_shape<1, 1>), stripes, 64, 0, 0, a, b, stripes);
+                if (kind == 2) hipLaunchKernelGGL((k_enc_shape<1, 1>), stripes / 4, 256, 0, 0, a, b, stripes);
+                if (kind == 3) hipLaunchKernelGGL((k_enc_shape<1, 2>), stripes, 64, 0, 0, a, b, stripes);
+                if (kind == 4) hipLaunchKernelGGL((k_enc_shape<4, 2>), stripes / 4, 64, 0, 0, a, b, stripes / 4);
+                if (kind == 5) hipLaunchKernelGGL((k_enc_shape<4, 1>), stripes / 16, 256, 0, 0, a, b, stripes / 4);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms;
+                hipEventElapsedTime(&ms, e0, e1);
+                if (rep && ms < bb) bb = ms;
+            }
+            const char *nm[] = {"4 stripes/wave, 256 rows", "1 stripe/wave, 1024 rows", "1 stripe/wave, WG 4 waves",
+                                "1 stripe/wave, 2048 rows", "4 stripes/wave, 512 rows", "4 stripes/wave, WG 4 waves"};
+            printf("enc-shape r1w2 %-28s %7.1f GB/s\n", nm[kind], 1.5 * bytes / bb / 1e6);
+        }
     }
     return 0;
 }
