@@ -230,31 +230,6 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     if (live)
         v = stripe_at(g, s);
 
-    // ---- packed product tables T_m, m = 1..K-1, for this lane's stripe
-    u32 coef[W];  // packed ids[i]^m
-    u32 idw[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-        u32 x = 0;
-        if (live)
-            for (int b = 0; b < 4; ++b)
-                if (4 * w + b < n)
-                    x |= u32(ids[u64(s) * n + 4 * w + b]) << (8 * b);
-        idw[w] = x;
-        coef[w] = x;
-    }
-    u8 *mytbl = tbl + gi * (K - 1) * TB;
-#pragma unroll
-    for (int m = 1; m < K; ++m) {
-        u32 basis[8][W];
-        make_basis<W>(basis, coef);
-        build_table<W, LP>(mytbl + (m - 1) * TB, basis, li);
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-            coef[w] = gf_mul_packed(coef[w], idw[w]);
-    }
-    __syncthreads();
-
     // ---- hash chain of this lane: part hi, accumulator ha
     const int hi = li >> 2, ha = li & 3;
     const bool hlane = HASH && live && hi < n;
@@ -289,8 +264,36 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
             }
         }
     };
+    // first chunk's rows requested before the tables are built: the HBM
+    // latency hides under the table build instead of following it
     if (nchunks && 16 * li < v.ps)
         load_task(16 * li);
+
+    // ---- packed product tables T_m, m = 1..K-1, for this lane's stripe
+    u32 coef[W];  // packed ids[i]^m
+    u32 idw[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        u32 x = 0;
+        if (live)
+            for (int b = 0; b < 4; ++b)
+                if (4 * w + b < n)
+                    x |= u32(ids[u64(s) * n + 4 * w + b]) << (8 * b);
+        idw[w] = x;
+        coef[w] = x;
+    }
+    u8 *mytbl = tbl + gi * (K - 1) * TB;
+#pragma unroll
+    for (int m = 1; m < K; ++m) {
+        u32 basis[8][W];
+        make_basis<W>(basis, coef);
+        build_table<W, LP>(mytbl + (m - 1) * TB, basis, li);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            coef[w] = gf_mul_packed(coef[w], idw[w]);
+    }
+    __syncthreads();
+
 
     // Software pipeline: iteration c encodes chunk c while the hash lanes run
     // the XXH64 rounds of chunk c-1 from registers (hw[]), so the serial
@@ -517,6 +520,37 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         cand_id[gi][li] = sid[sl];
     }
     __syncthreads();
+
+    // The first K offered slots are the selection unless an id repeats
+    // among them (crt/nk8.c:512-537): request the first step's rows from
+    // them now, so the HBM latency hides under the selection, the inverse
+    // and the table build; a changed selection reloads below.
+    const u32 B = g.block_size;
+    const u32 ps = part_size_of(B, K);
+    const u32 steps = (ps + R - 1) / R, per = VERIFY ? steps : (steps + slices - 1) / slices;
+    const u32 rend = VERIFY ? ps : min(ps, (slice + 1) * per * R);
+    const u32 rfirst = (VERIFY ? 0u : slice * per * R) + 16 * li;
+    u8 spec[K];
+    const u8 *src[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        spec[c] = (c < navail && c < LP) ? cand_slot[gi][c] : 0;
+        src[c] = g.parts + (u64(s) * n_slots + spec[c]) * g.part_pitch;
+    }
+    u32 pv[K][4];
+    auto load_step = [&](u32 r0) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
+            pv[c][0] = t.x;
+            pv[c][1] = t.y;
+            pv[c][2] = t.z;
+            pv[c][3] = t.w;
+        }
+    };
+    if (live && navail >= K && rfirst < rend)
+        load_step(rfirst);
+
     if (li == 0) {
         int h = 0;
         if (live) {
@@ -607,26 +641,16 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     if (!ok)
         return;
 
-    const u32 B = g.block_size;
-    const u32 ps = part_size_of(B, K);
-    const u8 *src[K];
+    bool respec = false;
 #pragma unroll
-    for (int c = 0; c < K; ++c)
+    for (int c = 0; c < K; ++c) {
+        respec |= slot[gi][c] != spec[c];
         src[c] = g.parts + (u64(s) * n_slots + slot[gi][c]) * g.part_pitch;
+    }
+    if (respec && rfirst < rend)
+        load_step(rfirst);
     u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
     const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
-
-    u32 pv[K][4];
-    auto load_step = [&](u32 r0) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
-            pv[c][0] = t.x;
-            pv[c][1] = t.y;
-            pv[c][2] = t.z;
-            pv[c][3] = t.w;
-        }
-    };
     auto rebuild = [&](u32 (&o)[4 * K]) {
         // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
         // bytes are packed into K output dwords with v_perm (<= 2 per dword)
@@ -674,12 +698,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     };
 
     if constexpr (!VERIFY) {
-        const u32 steps = (ps + R - 1) / R, per = (steps + slices - 1) / slices;
-        const u32 rend = min(ps, (slice + 1) * per * R);
-        u32 r0 = slice * per * R + 16 * li;
-        if (r0 < rend)
-            load_step(r0);
-        for (; r0 < rend; r0 += R) {
+        for (u32 r0 = rfirst; r0 < rend; r0 += R) {
             u32 o[4 * K];
             rebuild(o);
             if (r0 + R < rend)
@@ -696,12 +715,9 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         const int hc = li >> 2, ha = li & 3;
         const bool hlane = li < 4 * K;
         const u32 nst = ps >> 5;
-        const u32 steps = (ps + R - 1) / R;
         u64 acc = xxh_acc_init(ha, 0);
         u64 hw[RPC];
         int hvalid = 0;
-        if (16 * li < ps)
-            load_step(16 * li);
         for (u32 t = 0; t <= steps; ++t) {
             const u32 r0 = t * R + 16 * li;
             const bool act = t < steps && r0 < ps;
