@@ -97,6 +97,30 @@ int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off,
 		     const uint64_t *d_len, uint32_t count, uint64_t seed,
 		     uint64_t *d_out, void *stream);
 
+/* The core's per-cluster integrity sum, batched:
+ * d_sums[i] = XXH64 of the whole cluster d_clusters + i*cluster_pitch,
+ * cluster_size bytes, seed 0 -- dio_clu_sum / dio_pages_sum
+ * (core/dio.c:26-37,844-847), which hash every page of a 64 KiB cluster
+ * whatever part of it holds data.  With d_expect != NULL the compare of
+ * nkfs_inode_block_check_sum (core/inode.c:561-575) is fused in:
+ * d_status[i] = 0 when the sum matches d_expect[i], else -EINVAL.
+ * d_clusters and cluster_pitch must be multiples of 8. */
+int nkfs_clu_sum_batch(const uint8_t *d_clusters, uint64_t cluster_pitch,
+		       uint32_t cluster_size, uint32_t count,
+		       uint64_t *d_sums, const uint64_t *d_expect,
+		       int32_t *d_status, void *stream);
+
+/* nkfs_pages_dsum (core/upages.c:124-148), batched over page lists: payload
+ * i is the first d_len[i] bytes of the pages d_pages[d_first_page[i]],
+ * d_pages[d_first_page[i] + 1], ... (each page_size bytes, 8-byte aligned;
+ * the reference's pages are 4 KiB), hashed as one message -> d_dsums[i].
+ * The caller guarantees the page list covers d_len[i] (the reference's
+ * -EINVAL/BUG_ON checks, :131-139).  page_size: power of two >= 512. */
+int nkfs_pages_dsum_batch(const uint8_t *const *d_pages,
+			  const uint64_t *d_first_page, const uint64_t *d_len,
+			  uint32_t count, uint32_t page_size,
+			  uint64_t *d_dsums, void *stream);
+
 /* Host-memory form of nkfs_nk8_encode: blocks, ids, parts and digests in
  * host memory (the path's real entry: socket -> page buffers -> device,
  * SURVEY.md §8(f) row 2).  The batch is cut into sub-batches of about

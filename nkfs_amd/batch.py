@@ -158,6 +158,37 @@ def xxh64_batch(base: torch.Tensor, off: torch.Tensor, lens: torch.Tensor, seed:
     return out
 
 
+def clu_sum(clusters: torch.Tensor, cluster_size: int | None = None, expect: torch.Tensor | None = None,
+            stream=None):
+    """dio_clu_sum over every row of clusters (uint8 [count, pitch]): XXH64 of
+    the first cluster_size bytes (default: the whole row).  With expect
+    (int64 [count]) also returns the per-cluster status (0 / -EINVAL) of
+    nkfs_inode_block_check_sum.  Returns (sums, status|None)."""
+    _need(clusters, U8, "clusters")
+    count = clusters.shape[0]
+    size = clusters.shape[1] if cluster_size is None else cluster_size
+    sums = torch.empty(count, dtype=torch.int64, device=clusters.device)
+    status = None
+    if expect is not None:
+        _need(expect, torch.int64, "expect")
+        status = torch.empty(count, dtype=torch.int32, device=clusters.device)
+    check(lib().nkfs_clu_sum_batch(clusters.data_ptr(), clusters.stride(0), size, count, sums.data_ptr(),
+                                   _ptr(expect), _ptr(status), _stream(stream)), "nkfs_clu_sum_batch")
+    return sums, status
+
+
+def pages_dsum(pages: torch.Tensor, first_page: torch.Tensor, lens: torch.Tensor, page_size: int = 4096,
+               stream=None):
+    """nkfs_pages_dsum over page lists: pages int64 [npages] device pointers,
+    payload i = first lens[i] bytes of pages[first_page[i]:]."""
+    for t, nm in ((pages, "pages"), (first_page, "first_page"), (lens, "lens")):
+        _need(t, torch.int64, nm)
+    out = torch.empty(lens.numel(), dtype=torch.int64, device=lens.device)
+    check(lib().nkfs_pages_dsum_batch(pages.data_ptr(), first_page.data_ptr(), lens.data_ptr(), lens.numel(),
+                                      page_size, out.data_ptr(), _stream(stream)), "nkfs_pages_dsum_batch")
+    return out
+
+
 def synth(nstripes: int, block_size: int, pitch: int | None = None, seed: int | None = None, first: int = 0,
           device="cuda", stream=None) -> torch.Tensor:
     from .synth import SEED

@@ -47,6 +47,13 @@ int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v,
 int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 			    const uint64_t *len, uint32_t count, uint64_t seed,
 			    uint64_t *out, void *stream);
+int nkfs_fast_xxh64_strided(const uint8_t *base, uint64_t pitch,
+			    uint64_t len, uint32_t count, uint64_t *out,
+			    const uint64_t *expect, int32_t *status,
+			    void *stream);
+int nkfs_fast_xxh64_pages(const uint8_t *const *pages, const uint64_t *first,
+			  const uint64_t *len, uint32_t count,
+			  uint32_t page_shift, uint64_t *out, void *stream);
 int nkfs_launch_synth(uint8_t *blocks, uint64_t block_pitch,
 		      uint32_t block_size, uint32_t nstripes,
 		      uint64_t seed, uint64_t first_stripe, void *stream);

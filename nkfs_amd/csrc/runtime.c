@@ -305,6 +305,39 @@ int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off, const uint64_
 	return nkfs_launch_xxh64_batch(d_base, d_off, d_len, count, seed, d_out, stream);
 }
 
+int nkfs_clu_sum_batch(const uint8_t *d_clusters, uint64_t cluster_pitch, uint32_t cluster_size, uint32_t count,
+		       uint64_t *d_sums, const uint64_t *d_expect, int32_t *d_status, void *stream)
+{
+	if (!g_ready)
+		return -EAGAIN;
+	if (!count)
+		return 0;
+	if (!d_clusters || !d_sums || (d_expect && !d_status) || ((uintptr_t)d_clusters & 7) ||
+	    (count > 1 && (cluster_pitch < cluster_size || (cluster_pitch & 7))))
+		return -EINVAL;
+	return nkfs_fast_xxh64_strided(d_clusters, cluster_pitch, cluster_size, count, d_sums, d_expect, d_status,
+				       stream);
+}
+
+int nkfs_pages_dsum_batch(const uint8_t *const *d_pages, const uint64_t *d_first_page, const uint64_t *d_len,
+			  uint32_t count, uint32_t page_size, uint64_t *d_dsums, void *stream)
+{
+	uint32_t shift = 0;
+
+	if (!g_ready)
+		return -EAGAIN;
+	if (!count)
+		return 0;
+	if (!d_pages || !d_first_page || !d_len || !d_dsums)
+		return -EINVAL;
+	/* a 512-byte hashing chunk must never straddle two pages */
+	if (page_size < 512 || (page_size & (page_size - 1)))
+		return -EINVAL;
+	while ((1u << shift) < page_size)
+		shift++;
+	return nkfs_fast_xxh64_pages(d_pages, d_first_page, d_len, count, shift, d_dsums, stream);
+}
+
 int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
 		      uint64_t seed, uint64_t first_stripe, void *stream)
 {

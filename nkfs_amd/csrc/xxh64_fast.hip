@@ -30,24 +30,74 @@ constexpr int PIECES = MSGS * CH / 16; // 16-byte pieces per iteration
 constexpr int PPL = PIECES / 64;       // pieces per lane (8)
 constexpr int SPAD = CH + 32;          // LDS bytes per message (bank spread)
 
+// A message source maps message m to (descriptor, length) and a byte
+// offset inside the message to its address.  Every source guarantees that
+// an aligned 16-byte piece never straddles a discontinuity.
 struct MsgList {  // explicit (offset, length) list
+    typedef const u8 *Desc;
     const u8 *base;
     const u64 *off;
     const u64 *len;
     u32 count;
-    __device__ bool get(u32 m, const u8 *&p, u64 &n) const
+    __device__ bool get(u32 m, Desc &d, u64 &n) const
     {
         if (m >= count)
             return false;
-        p = base + off[m];
+        d = base + off[m];
         n = len[m];
         return true;
+    }
+    __device__ static const u8 *at(Desc d, u64 pos) { return d + pos; }
+};
+
+struct Strided {  // count messages of len bytes, pitch apart (clusters)
+    typedef const u8 *Desc;
+    const u8 *base;
+    u64 pitch;
+    u64 len;
+    u32 count;
+    __device__ bool get(u32 m, Desc &d, u64 &n) const
+    {
+        if (m >= count)
+            return false;
+        d = base + u64(m) * pitch;
+        n = len;
+        return true;
+    }
+    __device__ static const u8 *at(Desc d, u64 pos) { return d + pos; }
+};
+
+struct PageList {  // message m = first len[m] bytes of pages[first[m]..]
+    struct Desc {
+        const u8 *const *pg;
+        u32 shift;
+    };
+    const u8 *const *pages;
+    const u64 *first;
+    const u64 *len;
+    u32 count;
+    u32 shift;  // log2(page size), >= log2(CH)
+    __device__ bool get(u32 m, Desc &d, u64 &n) const
+    {
+        d.shift = shift;
+        if (m >= count) {
+            d.pg = nullptr;
+            return false;
+        }
+        d.pg = pages + first[m];
+        n = len[m];
+        return true;
+    }
+    __device__ static const u8 *at(Desc d, u64 pos)
+    {
+        return d.pg[pos >> d.shift] + (pos & ((u64(1) << d.shift) - 1));
     }
 };
 
 struct PartsOf {  // every part of a batch laid out by nkfs_geom
+    typedef const u8 *Desc;
     nkfs_geom g;
-    __device__ bool get(u32 m, const u8 *&p, u64 &n) const
+    __device__ bool get(u32 m, Desc &p, u64 &n) const
     {
         const u64 total = u64(g.nstripes) * u64(g.n);
         if (m >= total)
@@ -68,6 +118,7 @@ struct PartsOf {  // every part of a batch laid out by nkfs_geom
         n = ps;
         return true;
     }
+    __device__ static const u8 *at(Desc d, u64 pos) { return d + pos; }
 };
 
 __device__ inline u64 shfl64(u64 v, int src)
@@ -79,8 +130,11 @@ __device__ inline u64 shfl64(u64 v, int src)
 
 }  // namespace
 
+// expect != NULL: status[m] = 0 when out[m] == expect[m], else -EINVAL
+// (the compare of nkfs_inode_block_check_sum, core/inode.c:561-575).
 template <class Src>
-__global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out)
+__global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out, const u64 *expect,
+                                                   int32_t *status)
 {
     __shared__ __attribute__((aligned(16))) u8 buf[MSGS * SPAD];
     const int lane = threadIdx.x;
@@ -88,25 +142,21 @@ __global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out)
 
     // loader role: piece q of lane = message (lane + 64q) / 32, 16-B piece
     // (lane + 64q) % 32 of that message's chunk
-    const u8 *lp[PPL];
+    typename Src::Desc lp[PPL];
     u64 llen[PPL];
     int lmsg[PPL], lpos[PPL];
-    bool la16[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; ++q) {
         const int pc = lane + 64 * q;
         lmsg[q] = pc / (CH / 16);
         lpos[q] = (pc % (CH / 16)) * 16;
-        const u8 *p = nullptr;
         u64 n = 0;
-        src.get(m0 + lmsg[q], p, n);
-        lp[q] = p;
+        src.get(m0 + lmsg[q], lp[q], n);
         llen[q] = n;
-        la16[q] = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
     }
     // hash role: message hm, accumulator ha
     const int hm = lane >> 2, ha = lane & 3;
-    const u8 *hp = nullptr;
+    typename Src::Desc hp;
     u64 hlen = 0;
     const bool hlive = src.get(m0 + hm, hp, hlen);
     const u64 nst = hlen >> 5;
@@ -117,18 +167,21 @@ __global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out)
 #pragma unroll
         for (int q = 0; q < PPL; ++q) {
             const u64 pos = u64(c) * CH + lpos[q];
+            // at() may read a page table: only for bytes inside the message
             if (pos + 16 <= llen[q]) {
-                if (la16[q]) {
-                    d[q] = *reinterpret_cast<const uint4 *>(lp[q] + pos);
+                const u8 *a = Src::at(lp[q], pos);
+                if ((reinterpret_cast<uintptr_t>(a) & 15) == 0) {
+                    d[q] = *reinterpret_cast<const uint4 *>(a);
                 } else {  // 8-byte aligned (API contract)
-                    const u64 *w = reinterpret_cast<const u64 *>(lp[q] + pos);
-                    const u64 a = w[0], b = w[1];
-                    d[q] = make_uint4(u32(a), u32(a >> 32), u32(b), u32(b >> 32));
+                    const u64 *w = reinterpret_cast<const u64 *>(a);
+                    const u64 lo = w[0], hi = w[1];
+                    d[q] = make_uint4(u32(lo), u32(lo >> 32), u32(hi), u32(hi >> 32));
                 }
             } else if (pos < llen[q]) {
+                const u8 *a = Src::at(lp[q], pos);
                 u32 x[4] = {0, 0, 0, 0};
                 for (u32 b = 0; b < 16 && pos + b < llen[q]; ++b)
-                    x[b >> 2] |= u32(lp[q][pos + b]) << (8 * (b & 3));
+                    x[b >> 2] |= u32(a[b]) << (8 * (b & 3));
                 d[q] = make_uint4(x[0], x[1], x[2], x[3]);
             }
         }
@@ -192,7 +245,10 @@ __global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out)
             for (int w = 0; w < 4; ++w)
                 tw[w] = t[w];
         }
-        out[m0 + hm] = xxh_tail_regs(h, tw, left);
+        const u64 dig = xxh_tail_regs(h, tw, left);
+        out[m0 + hm] = dig;
+        if (expect)
+            status[m0 + hm] = dig == expect[m0 + hm] ? 0 : -EINVAL;
     }
 }
 
@@ -202,7 +258,8 @@ extern "C" int nkfs_fast_xxh64_list(const uint8_t *base, const uint64_t *off, co
     if (!count)
         return 0;
     MsgList src{base, off, len, count};
-    hipLaunchKernelGGL(k_xxh64_fast<MsgList>, dim3((count + MSGS - 1) / MSGS), dim3(64), 0, st, src, seed, out);
+    hipLaunchKernelGGL(k_xxh64_fast<MsgList>, dim3((count + MSGS - 1) / MSGS), dim3(64), 0, st, src, seed, out,
+                       (const u64 *)nullptr, (int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -213,6 +270,30 @@ extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, uint64_t *out, hipStrea
         return 0;
     PartsOf src{*g};
     hipLaunchKernelGGL(k_xxh64_fast<PartsOf>, dim3(u32((total + MSGS - 1) / MSGS)), dim3(64), 0, st, src,
-                       u64(0), out);
+                       u64(0), out, (const u64 *)nullptr, (int32_t *)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int nkfs_fast_xxh64_strided(const uint8_t *base, uint64_t pitch, uint64_t len, uint32_t count,
+                                       uint64_t *out, const uint64_t *expect, int32_t *status, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (!count)
+        return 0;
+    Strided src{base, pitch, len, count};
+    hipLaunchKernelGGL(k_xxh64_fast<Strided>, dim3((count + MSGS - 1) / MSGS), dim3(64), 0, st, src, u64(0), out,
+                       expect, status);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int nkfs_fast_xxh64_pages(const uint8_t *const *pages, const uint64_t *first, const uint64_t *len,
+                                     uint32_t count, uint32_t page_shift, uint64_t *out, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (!count)
+        return 0;
+    PageList src{pages, first, len, count, page_shift};
+    hipLaunchKernelGGL(k_xxh64_fast<PageList>, dim3((count + MSGS - 1) / MSGS), dim3(64), 0, st, src, u64(0), out,
+                       (const u64 *)nullptr, (int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -7,7 +7,8 @@ nk8_assemble_block) and crt/xxhash.c (XXH64) called through ctypes; inputs
 are regenerated from the seeded stripe synthesiser (nkfs_amd/synth.py), so
 the fixture holds only ids, digests and -- for small parts -- the part bytes.
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py          # everything (new random ids)
+    python tests/golden/gen_golden.py c1       # one section only
 """
 from __future__ import annotations
 
@@ -46,6 +47,24 @@ ERROR_CASES = [  # (block_size, n, k) that the reference rejects with -EINVAL
 
 def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def c1_section() -> dict:
+    """Config 1 user-space half: a 1 MiB + ragged object
+    moved in 64 KiB chunks (client/main.c:46); each chunk's payload dsum
+    (client/lib/client.c:146-148 == core/upages.c:124-148) and the whole-
+    cluster sum of the zero-padded 64 KiB block it lands in (core/dio.c:26-37)."""
+    obj_size, chunk = (1 << 20) + 12345, 65536
+    obj = synth.stripe_bytes(9000, obj_size)
+    dsums, clus = [], []
+    for off in range(0, obj_size, chunk):
+        piece = obj[off:off + chunk]
+        dsums.append(f"{O.ref_xxh64(piece):016x}")
+        clu = np.zeros(chunk, np.uint8)
+        clu[:piece.size] = piece
+        clus.append(f"{O.ref_xxh64(clu):016x}")
+    return {"stripe": 9000, "object_size": obj_size, "chunk": chunk, "chunk_dsums": dsums,
+            "cluster_sums": clus, "object_sha256": sha(obj)}
 
 
 def main() -> None:
@@ -99,12 +118,28 @@ def main() -> None:
     doc = {
         "generator": "tests/golden/gen_golden.py (reference crt/nk8.c + crt/xxhash.c via oracle/_ref)",
         "synth_seed": f"{synth.SEED:x}",
-        "encode": enc, "decode": dec, "split_errors": errs, "xxh64": xx,
+        "encode": enc, "decode": dec, "split_errors": errs, "xxh64": xx, "c1": c1_section(),
     }
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=0, sort_keys=True)
     print(f"wrote {OUT}: {len(enc)} encode, {len(dec)} decode, {len(errs)} error, {len(xx)} xxh64 cases")
 
 
+def refresh(sections: list[str]) -> None:
+    """Regenerate only the named sections, keeping the rest of the fixture
+    (the encode cases hold ids the reference drew at random)."""
+    makers = {"c1": c1_section}
+    with open(OUT) as f:
+        doc = json.load(f)
+    for name in sections:
+        doc[name] = makers[name]()
+    with open(OUT, "w") as f:
+        json.dump(doc, f, indent=0, sort_keys=True)
+    print(f"refreshed {sections} in {OUT}")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        refresh(sys.argv[1:])
+    else:
+        main()

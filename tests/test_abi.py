@@ -72,6 +72,8 @@ def test_no_gpu_fails_loudly():
     pi = u8p()
     assert L.nk8_split_block(buf, 4096, 4, 2, C.byref(pp), C.byref(pi)) == -11  # -EAGAIN
     assert L.nkfs_nk8_encode(None, 4096, 4096, 1, 4, 2, None, None, 2048, None, None) == -11
+    assert L.nkfs_clu_sum_batch(None, 65536, 65536, 1, None, None, None, None) == -11
+    assert L.nkfs_pages_dsum_batch(None, None, None, 1, 4096, None, None) == -11
     assert L.nkfs_dev_alloc(16) is None
 
 

@@ -80,6 +80,21 @@ def test_xxh64_vectors(golden):
         assert xxhash.xxh64_intdigest(data.tobytes(), seed) == want  # independent implementation
 
 
+def test_c1_chunk_and_cluster_sums(golden):
+    """Config 1's user-space sums (client chunk dsum, zero-padded cluster sum)
+    as computed by the reference, against the oracle and the xxhash module."""
+    c1 = golden["c1"]
+    obj = synth.stripe_bytes(c1["stripe"], c1["object_size"])
+    assert sha(obj) == c1["object_sha256"]
+    ch = c1["chunk"]
+    for i, off in enumerate(range(0, obj.size, ch)):
+        piece = obj[off:off + ch]
+        assert f"{O.xxh64(piece):016x}" == c1["chunk_dsums"][i]
+        clu = np.zeros(ch, np.uint8)
+        clu[:piece.size] = piece
+        assert f"{xxhash.xxh64_intdigest(clu.tobytes()):016x}" == c1["cluster_sums"][i]
+
+
 def test_gf_table_is_the_aes_field():
     t = O.gf_mul_table()
     assert t[0x57, 0x83] == 0xC1  # FIPS-197 4.2 worked example, poly 0x11B

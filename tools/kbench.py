@@ -1,6 +1,6 @@
 """Kernel-level timing of the nkfs device entry points (ablation helper).
 
-    python tools/kbench.py [c2 c3 c4 ...]
+    python tools/kbench.py [c2 c3 c4 clu ...]
 
 For each config: encode+hash, encode alone (d_digests = NULL), decode, and
 the batched XXH64 of the parts, each averaged over per-launch HIP event
@@ -32,10 +32,39 @@ def timeit(fn, reps=20):
     return t[len(t) // 2] / 1e3
 
 
+def clusters(count=16384, ch=65536, page=4096):
+    """Integrity shapes: whole-cluster sums and 4 KiB page-list dsums."""
+    d = batch.synth(count, ch)
+    t = timeit(lambda: batch.clu_sum(d))
+    print(f"clu  sum x{count}   {t*1e6:9.1f} us {count*ch/t/1e9:7.1f} GB/s")
+    exp, _ = batch.clu_sum(d)
+    t = timeit(lambda: batch.clu_sum(d, expect=exp))
+    print(f"clu  check         {t*1e6:9.1f} us {count*(ch+8)/t/1e9:7.1f} GB/s")
+    npg = count * ch // page
+    g = torch.Generator().manual_seed(1)
+    perm = torch.randperm(npg, generator=g).cuda()
+    ptrs = d.data_ptr() + perm.to(torch.int64) * page
+    first = torch.arange(count, device="cuda", dtype=torch.int64) * (ch // page)
+    lens = torch.full((count,), ch, device="cuda", dtype=torch.int64)
+    t = timeit(lambda: batch.pages_dsum(ptrs, first, lens, page))
+    print(f"pages dsum scat.   {t*1e6:9.1f} us {count*ch/t/1e9:7.1f} GB/s")
+
+
 def main():
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(0))
     for name in sys.argv[1:] or ["c2", "c4"]:
+        if name == "clu":
+            clusters()
+            continue
+        if name == "cluvar":  # wave count vs power-of-two stride
+            for count, ch, pitch in ((16384, 65536, 65536), (16384, 65536, 65536 + 256), (65536, 16384, 16384),
+                                     (65536, 16384, 16384 + 256), (131072, 8192, 8192), (4096, 262144, 262144)):
+                d = torch.empty((count, pitch), dtype=torch.uint8, device="cuda")
+                t = timeit(lambda: batch.clu_sum(d, cluster_size=ch))
+                print(f"clu {count:6d} x {ch:6d} pitch {pitch:6d} {t*1e6:9.1f} us {count*ch/t/1e9:7.1f} GB/s")
+                del d
+            continue
         S, B, n, k, _ = CONFIGS[name]
         ps = batch.part_size(B, k)
         blocks = batch.synth(S, B)
