@@ -457,7 +457,7 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
 
 // ------------------------------------------------------------------ decode
 //
-// One wave = G stripes (G = 1 by default; 4 for k <= 4 as an A/B form),
+// One wave = G stripes (G = 1 as launched; the kernel also takes G = 2, 4),
 // k <= 8 (crt/nk8.c:446-599):
 //  1. lane 0 of each stripe picks the first k offered parts with distinct ids
 //     (crt/nk8.c:512-537) and forms M(t) = prod_c (t + x_c);
@@ -465,9 +465,8 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
 //     in closed form (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) divided
 //     by M'(x_c)), the unique inverse the reference's Gauss-Jordan produces;
 //  3. packed tables U_c[x] = (W[c][0]*x, ..., W[c][k-1]*x) go to LDS;
-//  4. every lane rebuilds U x 16 rows per step: per 16-row unit one 16-byte
-//     load from each of the k parts, k*16 lookups, rows packed back to k*16
-//     contiguous bytes:
+//  4. every lane rebuilds 16 rows per step: one 16-byte load from each of the
+//     k parts, k*16 lookups, rows packed back to k*16 contiguous bytes:
 //       block[j*k + m] = XOR_c part_c[j] * W[c][m]      (crt/nk8.c:552-582)
 //     with the next step's loads issued before this step's stores.
 namespace {
@@ -486,15 +485,13 @@ __device__ inline u32 gfm(u32 a, u32 b)
 
 }  // namespace
 
-template <int K, int E, int G, int U, bool VERIFY>
+template <int K, int E, int G, bool VERIFY>
 __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
                                                     int navail, int32_t *status, const u8 *inv, bool nt, int slices,
                                                     const u64 *expect, u64 *badmask)
 {
     constexpr int LP = 64 / G;
-    constexpr int UR = 16 * LP;  // rows per 16-row unit of every lane
-    constexpr int R = UR * U;    // rows per stripe per step
-    static_assert(!VERIFY || U == 1, "the verifying form hashes one unit per step");
+    constexpr int R = 16 * LP;  // rows per stripe per step
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
     constexpr int SPX = R + 32;  // verify exchange buffer bytes per part
@@ -540,20 +537,15 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         spec[c] = (c < navail && c < LP) ? cand_slot[gi][c] : 0;
         src[c] = g.parts + (u64(s) * n_slots + spec[c]) * g.part_pitch;
     }
-    u32 pv[U][K][4];
+    u32 pv[K][4];
     auto load_step = [&](u32 r0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // pitch >= round16(ps); a unit past the part reloads row 0 (unused)
-            const u32 ru = r0 + u32(u) * UR < ps ? r0 + u32(u) * UR : 0u;
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + ru);
-                pv[u][c][0] = t.x;
-                pv[u][c][1] = t.y;
-                pv[u][c][2] = t.z;
-                pv[u][c][3] = t.w;
-            }
+        for (int c = 0; c < K; ++c) {
+            const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
+            pv[c][0] = t.x;
+            pv[c][1] = t.y;
+            pv[c][2] = t.z;
+            pv[c][3] = t.w;
         }
     };
     if (live && navail >= K && rfirst < rend)
@@ -659,7 +651,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         load_step(rfirst);
     u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
     const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
-    auto rebuild = [&](u32 (&o)[4 * K], int u) {
+    auto rebuild = [&](u32 (&o)[4 * K]) {
         // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
         // bytes are packed into K output dwords with v_perm (<= 2 per dword)
 #pragma unroll
@@ -673,7 +665,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                     row[rr * W + w] = 0;
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    const u32 byte = (pv[u][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                    const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
                     const u8 *e = mytbl + c * TB + byte * E;
                     if constexpr (E == 8) {
                         const uint2 t = *reinterpret_cast<const uint2 *>(e);
@@ -707,16 +699,11 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 
     if constexpr (!VERIFY) {
         for (u32 r0 = rfirst; r0 < rend; r0 += R) {
-            u32 o[U][4 * K];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                rebuild(o[u], u);
+            u32 o[4 * K];
+            rebuild(o);
             if (r0 + R < rend)
                 load_step(r0 + R);  // prefetch the next step under this one's stores
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (r0 + u32(u) * UR < rend)
-                    emit(o[u], r0 + u32(u) * UR);
+            emit(o, r0);
         }
     } else {
         // Integrity-checked decode: the k parts read for the rebuild are also
@@ -736,7 +723,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
             const bool act = t < steps && r0 < ps;
             u32 o[4 * K];
             if (act)
-                rebuild(o, 0);
+                rebuild(o);
 #pragma unroll
             for (int r = 0; r < RPC; ++r) {
                 const u64 nxt = xxh_round(acc, hw[r]);
@@ -746,7 +733,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
                 for (int c = 0; c < K; ++c)
                     *reinterpret_cast<uint4 *>(xbuf + (gi * K + c) * SPX + 16 * li) =
-                        make_uint4(pv[0][c][0], pv[0][c][1], pv[0][c][2], pv[0][c][3]);
+                        make_uint4(pv[c][0], pv[c][1], pv[c][2], pv[c][3]);
                 if (r0 + R < ps)
                     load_step(r0 + R);
                 emit(o, r0);
@@ -796,22 +783,19 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
         return -ENOSYS;
+    // one stripe per wave: for k 5..8 it halves the E=8 tables and lifts
+    // occupancy (C3 decode 3.27 -> 4.03 TB/s over two stripes per wave); for
+    // k <= 4 the wave then streams one stripe's parts in 1 KiB runs (C2
+    // decode 4.48 -> 5.08 TB/s over four stripes per wave, tools/ab_lib.py).
     const GfTables *t = (const GfTables *)gf;
     const bool nt = store_nt();
     const bool verify = expect != nullptr;
-    // one stripe per wave (C2 decode 4.48 -> 5.10 TB/s over four stripes per
-    // wave, tools/ab_env.py): the whole wave streams one stripe's parts in
-    // 1 KiB runs.  A/B knobs: NKFS_DEC_G=4 (k <= 4 four stripes per wave),
-    // NKFS_DEC_U=2 (two 16-row units per lane per step).
-    const char *dge = getenv("NKFS_DEC_G");
-    const char *due = getenv("NKFS_DEC_U");
-    const int G = (g->k <= 4 && dge && atoi(dge) == 4) ? 4 : 1;
-    const int U = (!verify && g->k <= 4 && due && atoi(due) == 2) ? 2 : 1;  // k > 4: U = 2 spills
+    const int G = 1;
     const u32 groups = (g->nstripes + G - 1) / G;
     // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4
     // steps; the verifying form hashes each part in order: one slice
     const u32 ps = g->block_size / u32(g->k) + (g->block_size % u32(g->k) ? 1u : 0u);
-    const u32 R = 16u * (64u / u32(G)) * u32(U);
+    const u32 R = 16u * (64u / u32(G));
     const u32 steps = (ps + R - 1) / R;
     u32 slices = 1;
     while (!verify && groups * slices < 4096u && steps / (slices * 2) >= 4)
@@ -820,34 +804,21 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
 #define NKFS_DK(KK, EE, GG)                                                                                     \
     do {                                                                                                        \
         if (verify)                                                                                             \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, true>), grid, dim3(64), 0, st, *g, n_slots, ids,    \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
-        else if (U == 2)                                                                                        \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64), 0, st, *g, n_slots, ids,   \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, false>), grid, dim3(64), 0, st, *g, n_slots, ids,   \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
-    } while (0)
-#define NKFS_DK1(KK)                                                                                            \
-    do {                                                                                                        \
-        if (verify)                                                                                             \
-            hipLaunchKernelGGL((k_decode_fast<KK, 8, 1, 1, true>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, true>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, \
                                navail, status, t->inv, nt, int(slices), expect, badmask);                       \
         else                                                                                                    \
-            hipLaunchKernelGGL((k_decode_fast<KK, 8, 1, 1, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, false>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
                                avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
     } while (0)
     switch (g->k) {
-    case 2: if (G == 4) NKFS_DK(2, 4, 4); else NKFS_DK(2, 4, 1); break;
-    case 3: if (G == 4) NKFS_DK(3, 4, 4); else NKFS_DK(3, 4, 1); break;
-    case 4: if (G == 4) NKFS_DK(4, 4, 4); else NKFS_DK(4, 4, 1); break;
-    case 5: NKFS_DK1(5); break;
-    case 6: NKFS_DK1(6); break;
-    case 7: NKFS_DK1(7); break;
-    case 8: NKFS_DK1(8); break;
+    case 2: NKFS_DK(2, 4, 1); break;
+    case 3: NKFS_DK(3, 4, 1); break;
+    case 4: NKFS_DK(4, 4, 1); break;
+    case 5: NKFS_DK(5, 8, 1); break;
+    case 6: NKFS_DK(6, 8, 1); break;
+    case 7: NKFS_DK(7, 8, 1); break;
+    case 8: NKFS_DK(8, 8, 1); break;
 #undef NKFS_DK
-#undef NKFS_DK1
     default:
         return -ENOSYS;
     }
