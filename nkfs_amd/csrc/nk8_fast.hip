@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "nk8_dev.h"
 #include "gf256.h"
 #include "nkfs_internal.h"
 #include "xxh64_dev.h"
@@ -36,179 +37,12 @@ typedef uint8_t u8;
 typedef uint32_t u32;
 typedef uint64_t u64;
 
-namespace {
+using namespace nkfs::dev;
 
-__device__ inline u32 part_size_of(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
-
-// per-byte GF product of two packed words (a_i * b_i for each byte i)
-__device__ inline u32 gf_mul_packed(u32 a, u32 b)
-{
-    u32 r = 0;
-#pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-        const u32 mask = ((b >> bit) & 0x01010101u) * 0xFFu;
-        r ^= a & mask;
-        a = gf_xtime4(a);
-    }
-    return r;
-}
-
-// Fill a 256-entry packed product table T[x] = XOR_{bit b of x} basis[b]
-// (multiplication by a constant is GF(2)-linear) with the LP lanes of one
-// stripe: lane li owns entries x = li + LP*j, walks j in Gray-code order and
-// pays one XOR per entry and word; consecutive lanes write consecutive
-// entries, so the LDS stores are conflict-free.
-template <int W, int LP>
-__device__ inline void build_table(u8 *t, const u32 (&basis)[8][W], int li)
-{
-    constexpr int LB = LP == 16 ? 4 : LP == 32 ? 5 : 6;
-    static_assert(LP == 16 || LP == 32 || LP == 64, "lanes per stripe");
-    u32 hv[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-        u32 e = 0;
-#pragma unroll
-        for (int b = 0; b < LB; ++b)
-            e ^= basis[b][w] & (0u - ((u32(li) >> b) & 1u));
-        hv[w] = e;
-    }
-#pragma unroll
-    for (int j = 0; j < 256 / LP; ++j) {
-        if (j) {
-            const int bit = __builtin_ctz(j);
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                hv[w] ^= basis[LB + bit][w];
-        }
-        const int x = li + LP * (j ^ (j >> 1));
-        if constexpr (W == 2)
-            *reinterpret_cast<uint2 *>(t + x * 8) = make_uint2(hv[0], hv[1]);
-        else
-            *reinterpret_cast<u32 *>(t + x * 4) = hv[0];
-    }
-}
-
-// basis[b] = packed coefficient row * 2^b (b = 0..7)
-template <int W>
-__device__ inline void make_basis(u32 (&basis)[8][W], const u32 (&row)[W])
-{
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-        u32 x = row[w];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            basis[b][w] = x;
-            x = gf_xtime4(x);
-        }
-    }
-}
-
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-
-// 16-byte store, plain or non-temporal (global_store_dwordx4 ... nt): the
-// parts/blocks are written once and not read again by this kernel
-__device__ inline void store16(void *p, u32 a, u32 b, u32 c, u32 d, bool nt)
-{
-    const v4u v = {a, b, c, d};
-    if (nt)
-        __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
-    else
-        *reinterpret_cast<v4u *>(p) = v;
-}
-
-// Output dword q (bytes 4q..4q+3) of 4 consecutive K-byte rows, each row
-// held in W dwords of `row` (row r, byte m at row[r*W + m/4] byte m%4).
-// The <= 3 distinct source dwords are merged with one or two v_perm_b32.
-template <int K, int W>
-__device__ __forceinline__ u32 pack_dword(const u32 *row, int q)
-{
-    int src[4], byt[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int p = 4 * q + b, r = p / K, m = p % K;
-        src[b] = r * W + (m >> 2);
-        byt[b] = m & 3;
-    }
-    // distinct sources in first-use order
-    int d0 = src[0], d1 = -1, d2 = -1;
-#pragma unroll
-    for (int b = 1; b < 4; ++b) {
-        if (src[b] != d0 && d1 < 0)
-            d1 = src[b];
-        else if (src[b] != d0 && src[b] != d1 && d2 < 0)
-            d2 = src[b];
-    }
-    u32 sel = 0;
-    if (d1 < 0) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            sel |= u32(byt[b]) << (8 * b);
-        return __builtin_amdgcn_perm(row[d0], row[d0], sel);
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-        sel |= u32(src[b] == d0 ? byt[b] : 4 + byt[b]) << (8 * b);
-    const u32 t = __builtin_amdgcn_perm(row[d1], row[d0], sel);
-    if (d2 < 0)
-        return t;
-    u32 sel2 = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-        sel2 |= u32(src[b] == d2 ? 4 + byt[b] : b) << (8 * b);
-    return __builtin_amdgcn_perm(row[d2], t, sel2);
-}
-
-// 4x4 byte transpose: in[r] byte c -> out[c] byte r
-__device__ inline void transpose4(u32 a, u32 b, u32 c, u32 d, u32 &o0, u32 &o1, u32 &o2, u32 &o3)
-{
-    // v_perm_b32(S0, S1, sel): selector 0-3 -> S1 bytes, 4-7 -> S0 bytes
-    const u32 t0 = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
-    const u32 t1 = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
-    const u32 t2 = __builtin_amdgcn_perm(d, c, 0x05010400u);  // c0 d0 c1 d1
-    const u32 t3 = __builtin_amdgcn_perm(d, c, 0x07030602u);  // c2 d2 c3 d3
-    o0 = __builtin_amdgcn_perm(t2, t0, 0x05040100u);         // a0 b0 c0 d0
-    o1 = __builtin_amdgcn_perm(t2, t0, 0x07060302u);         // a1 b1 c1 d1
-    o2 = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
-    o3 = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
-}
-
-__device__ inline u64 shfl64(u64 v, int src)
-{
-    u32 lo = __shfl(u32(v), src, 64);
-    u32 hi = __shfl(u32(v >> 32), src, 64);
-    return (u64(hi) << 32) | lo;
-}
-
-struct Stripe {
-    const u8 *blk;
-    u8 *parts;
-    u64 pitch;
-    u32 B;
-    u32 ps;
-};
-
-__device__ inline Stripe stripe_at(const nkfs_geom &g, u32 s)
-{
-    Stripe v;
-    if (g.block_sizes) {
-        v.B = g.block_sizes[s];
-        v.blk = g.blocks + g.block_off[s];
-        v.parts = g.parts + g.part_off[s];
-        v.ps = part_size_of(v.B, g.k);
-        v.pitch = (u64(v.ps) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
-    } else {
-        v.B = g.block_size;
-        v.blk = g.blocks + u64(s) * g.block_pitch;
-        v.parts = g.parts + u64(s) * u64(g.n) * g.part_pitch;
-        v.ps = part_size_of(v.B, g.k);
-        v.pitch = g.part_pitch;
-    }
-    return v;
-}
-
-}  // namespace
-
-template <int K, int E, bool HASH>
+// P = chunks of rows in flight per lane (prefetch depth, rotating register
+// slots): grids with few waves per SIMD (big stripes) cannot hide HBM
+// latency behind other waves, so each wave keeps more of its own loads out.
+template <int K, int E, int P, bool HASH>
 __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
     constexpr int G = E == 4 ? 4 : 2;   // stripes per wave
@@ -238,8 +72,8 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     const u32 nchunks = live ? (v.ps + R - 1) / R : 0;
     const bool aligned = ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
 
-    u32 d[4 * K];
-    auto load_task = [&](u32 r0) {
+    u32 dq[P][4 * K];
+    auto load_task = [&](u32 (&d)[4 * K], u32 r0) {
         const u64 off = u64(r0) * K;
         if (aligned && off + 16 * K <= v.B) {
             const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
@@ -264,10 +98,12 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
             }
         }
     };
-    // first chunk's rows requested before the tables are built: the HBM
-    // latency hides under the table build instead of following it
-    if (nchunks && 16 * li < v.ps)
-        load_task(16 * li);
+    // the first P chunks' rows are requested before the tables are built: the
+    // HBM latency hides under the table build instead of following it
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+        if (u32(p) < nchunks && p * R + 16 * li < v.ps)
+            load_task(dq[p], p * R + 16 * li);
 
     // ---- packed product tables T_m, m = 1..K-1, for this lane's stripe
     u32 coef[W];  // packed ids[i]^m
@@ -294,14 +130,13 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     }
     __syncthreads();
 
-
-    // Software pipeline: iteration c encodes chunk c while the hash lanes run
-    // the XXH64 rounds of chunk c-1 from registers (hw[]), so the serial
-    // multiply chain overlaps the table lookups instead of following them.
+    // Software pipeline: step c encodes chunk c while the hash lanes run the
+    // XXH64 rounds of chunk c-1 from registers (hw[]), so the serial multiply
+    // chain overlaps the table lookups instead of following them.
     constexpr int RPC = R / 32;  // rounds per chain per chunk
     u64 hw[RPC];
     int hvalid = 0;              // rounds pending in hw[]
-    for (u32 c = 0; __any(nchunks && c <= nchunks); ++c) {
+    auto step = [&](u32 (&d)[4 * K], u32 c) {
         const u32 r0 = c * R + 16 * li;
         const bool act = c < nchunks && r0 < v.ps;
         u32 row[16][W];
@@ -336,9 +171,10 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
             }
         }
         if (act) {
-            // prefetch the next chunk's rows while this one is stored
-            if (c + 1 < nchunks && r0 + R < v.ps)
-                load_task(r0 + R);
+            // this slot's rows are consumed: refill it with chunk c+P while
+            // this chunk is stored
+            if (c + P < nchunks && r0 + P * R < v.ps)
+                load_task(d, r0 + P * R);
             // rows -> parts: out[i][q] = bytes of part i for rows 4q..4q+3
             u32 out[E][4];
 #pragma unroll
@@ -375,9 +211,15 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
                     hw[rr] = *reinterpret_cast<const u64 *>(src + 32 * rr);
             }
             __syncthreads();
-        } else if (c >= nchunks) {
-            break;
         }
+    };
+    // with HASH one step past the last chunk folds its words; steps past a
+    // stripe's end are no-ops, so the P-unrolled body needs no exit inside
+    const u32 last = HASH ? nchunks : (nchunks ? nchunks - 1 : 0);
+    for (u32 c = 0; __any(nchunks && c <= last); c += P) {
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            step(dq[p], c + p);
     }
 
     if constexpr (HASH) {
@@ -409,13 +251,15 @@ static bool store_nt()
     return e ? atoi(e) != 0 : false;
 }
 
-template <int E, bool HASH>
-static int launch_k(int k, dim3 grid, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
+template <int E, int P, bool HASH>
+static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
 {
+    constexpr int G = E == 4 ? 4 : 2;
+    const dim3 grid((g.nstripes + G - 1) / G);
     switch (k) {
-#define NKFS_K(KK)                                                                        \
-    case KK:                                                                              \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, HASH>), grid, dim3(64), 0, st, g, ids, dig, nt); \
+#define NKFS_K(KK)                                                                                  \
+    case KK:                                                                                        \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH>), grid, dim3(64), 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -430,6 +274,19 @@ static int launch_k(int k, dim3 grid, hipStream_t st, const nkfs_geom &g, const 
     }
 }
 
+template <int E, bool HASH>
+static int launch_p(int P, int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
+{
+    switch (P) {
+    case 1: return launch_k<E, 1, HASH>(k, st, g, ids, dig, nt);
+    case 2: return launch_k<E, 2, HASH>(k, st, g, ids, dig, nt);
+    default: return launch_k<E, 3, HASH>(k, st, g, ids, dig, nt);
+    }
+}
+
+extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int ne, bool nt,
+                              hipStream_t st);
+
 // Returns -ENOSYS when the shape is outside the fast path (the caller then
 // uses the generic kernels).
 extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *,
@@ -440,16 +297,17 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     if (g->n > 8 || g->k > 8)
         return -ENOSYS;
     const int E = g->n <= 4 ? 4 : 8;
-    const int G = E == 4 ? 4 : 2;
-    const dim3 grid((g->nstripes + G - 1) / G);
     const bool nt = store_nt();
-    int rc;
-    if (E == 4)
-        rc = digests ? launch_k<4, true>(g->k, grid, st, *g, ids, digests, nt)
-                     : launch_k<4, false>(g->k, grid, st, *g, ids, digests, nt);
-    else
-        rc = digests ? launch_k<8, true>(g->k, grid, st, *g, ids, digests, nt)
-                     : launch_k<8, false>(g->k, grid, st, *g, ids, digests, nt);
+    const char *ws = getenv("NKFS_ENC_WS");  // experiment: warp-specialised kernel, value = encoder waves
+    if (ws && atoi(ws) > 0 && digests)
+        return nkfs_ws_encode(g, ids, digests, atoi(ws), nt, st);
+    int P = 1;
+    if (const char *e = getenv("NKFS_ENC_PREFETCH"))  // experiment: prefetch depth
+        P = atoi(e);
+    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, g->k, st, *g, ids, digests, nt)
+                                     : launch_p<4, false>(P, g->k, st, *g, ids, digests, nt))
+                          : (digests ? launch_p<8, true>(P, g->k, st, *g, ids, digests, nt)
+                                     : launch_p<8, false>(P, g->k, st, *g, ids, digests, nt));
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -797,8 +655,10 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     const u32 ps = g->block_size / u32(g->k) + (g->block_size % u32(g->k) ? 1u : 0u);
     const u32 R = 16u * (64u / u32(G));
     const u32 steps = (ps + R - 1) / R;
-    u32 slices = 1;
-    while (!verify && groups * slices < 4096u && steps / (slices * 2) >= 4)
+    u32 slices = 1, target = 4096;
+    if (const char *e = getenv("NKFS_DEC_WAVES"))  // experiment: wave-count target
+        target = u32(atoi(e));
+    while (!verify && groups * slices < target && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
 #define NKFS_DK(KK, EE, GG)                                                                                     \
