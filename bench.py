@@ -35,7 +35,11 @@ CONFIGS = {
     "c2": (65536, 4096, 4, 2, "C2: N=4,K=2 encode(+XXH64/part)+decode(2 erased), 65536 x 4 KiB stripes per GPU"),
     "c3": (2048, 1048576, 8, 5, "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 2048 x 1 MiB stripes per GPU"),
     "c4": (16384, 262144, 8, 5, "C4: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 16384 x 256 KiB stripes per GPU"),
+    # ragged: block size of every stripe drawn from C5_SIZES (synth.mixed_sizes)
+    "c5": (11520, None, 8, 5, "C5: N=8,K=5 encode(+XXH64/part)+decode(3 erased) of a ragged batch, stripe sizes "
+                              "uniform over {4 KiB, 64 KiB, 1 MiB}, 11520 stripes (~4 GiB) per GPU"),
 }
+C5_SIZES = (4096, 65536, 1048576)
 
 
 def parse():
@@ -114,6 +118,8 @@ def main():
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(local), "nkfs_gpu_init")
 
+    if args.config == "c5":
+        return run_ragged(args, rank, world, device)
     S, B, n, k, desc = CONFIGS[args.config]
     first, _ = stripe_range(rank, S)
     ps = batch.part_size(B, k)
@@ -215,6 +221,144 @@ def main():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def run_ragged(args, rank, world, device):
+    """C5: one ragged batch of mixed 4 KiB / 64 KiB / 1 MiB stripes, packed
+    back to back in HBM (block s at block_off[s], parts at part_off[s] with
+    the 256-B part pitch), encoded (+XXH64 of every part) with
+    nkfs_nk8_encode_ragged and decoded from n-k erased with
+    nkfs_nk8_decode_ragged each step."""
+    import numpy as np
+    import torch
+    from nkfs_amd import batch, synth
+
+    S, _, n, k, desc = CONFIGS["c5"]
+    first, _ = stripe_range(rank, S)
+    sizes = synth.mixed_sizes(first + S, C5_SIZES)[first:]
+    boff = np.zeros(S, np.int64)
+    poff = np.zeros(S, np.int64)
+    pos = ppos = 0
+    for s, B in enumerate(sizes.tolist()):
+        boff[s], poff[s] = pos, ppos
+        pos += (B + 255) // 256 * 256
+        ppos += n * batch.part_pitch(B, k)
+    stream = torch.cuda.current_stream(device)
+    # every stripe generated on the device (synth.stripe_bytes of its global
+    # index, cut to its size) and packed back to back
+    blocks = torch.zeros(pos, dtype=torch.uint8, device=device)
+    for s, B in enumerate(sizes.tolist()):
+        blocks[boff[s]: boff[s] + B].copy_(batch.synth(1, B, first=first + s, device=device)[0, :B])
+    ids_np = synth.batch_ids(S, n, first=first)
+    ids = torch.from_numpy(ids_np).to(device)
+    avail = torch.from_numpy(synth.batch_survivors(S, n, k, first=first)).to(device)
+    sz = torch.from_numpy(sizes.astype(np.int32)).to(device)
+    bo = torch.from_numpy(boff).to(device)
+    po = torch.from_numpy(poff).to(device)
+    parts = torch.empty(ppos, dtype=torch.uint8, device=device)
+    digests = torch.empty(S * n, dtype=torch.int64, device=device)
+    out = torch.zeros(pos, dtype=torch.uint8, device=device)
+    work = batch.decode_workspace(S, k, device)
+    status = torch.empty(S, dtype=torch.int32, device=device)
+    maxB = int(sizes.max())
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(e=None):
+        if e:
+            e[0].record(stream)
+        batch.encode_ragged(blocks, bo, sz, n, k, ids, parts, po, digests, maxB, stream=stream)
+        if e:
+            e[1].record(stream)
+        batch.decode_ragged(parts, po, n, ids, avail, k, out, bo, sz, maxB, work=work, status=status, stream=stream)
+        if e:
+            e[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(ev[i])
+    torch.cuda.synchronize(device)
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = reduce_max(t1 - t0, device)
+    enc_s = sum(e[0].elapsed_time(e[1]) for e in ev) / 1e3 / args.steps
+    dec_s = sum(e[1].elapsed_time(e[2]) for e in ev) / 1e3 / args.steps
+
+    ok = bool(torch.equal(out, blocks)) and int(status.abs().sum()) == 0
+    dig = [int(x) & 0xFFFFFFFFFFFFFFFF for x in digests.cpu().tolist()]
+    from oracle import oracle as O
+    for B in C5_SIZES:  # oracle digests on a sample of every size class
+        for s in np.nonzero(sizes == B)[0][:4].tolist():
+            blk = blocks[boff[s]: boff[s] + B].cpu().numpy()
+            ok &= dig[s * n:(s + 1) * n] == [O.xxh64(p) for p in O.encode(blk, n, k, ids_np[s])]
+    dx = 0
+    for d in dig:
+        dx ^= d
+    gathered = gather_digest_xor(dx, device)
+    ps = [batch.part_size(B, k) for B in sizes.tolist()]
+    user = int(sizes.sum())
+    enc_bytes = user + n * sum(ps) + 8 * n * S
+    dec_bytes = k * sum(ps) + user + k * S
+    value = user * world * args.steps / elapsed / 2**30
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846; sizes from the "
+                "separate size stream)",
+        "config": {"workload": desc, "n": n, "k": k, "block_sizes": list(C5_SIZES), "stripes_per_gpu": S,
+                   "user_bytes_per_gpu": user, "erased_per_stripe": n - k,
+                   "parallelism": f"stripe-partition x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "nkfs_nk8_encode_ragged (encode + XXH64 per part)",
+                     "achieved": round(enc_bytes / enc_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(enc_bytes / enc_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c5"),
+                     "bytes_per_launch": enc_bytes, "us_per_launch": round(enc_s * 1e6, 2)},
+        "decode": {"achieved_GBps": round(dec_bytes / dec_s / 1e9, 1), "us_per_launch": round(dec_s * 1e6, 2),
+                   "bytes_per_launch": dec_bytes},
+        "verified": ok,
+        "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline_mixed(sizes, n, k, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def cpu_baseline_mixed(sizes, n, k, target_s):
+    """The reference's split + XXH64 + assemble on a bounded sample of the
+    C5 mix: per size class, a few stripes timed until the class's share
+    (by bytes in the batch) of ~target_s is spent; GiB/s over the mix."""
+    from nkfs_amd import synth
+    from oracle import oracle as O
+    kind = "reference" if O.ref_lib() is not None else "port"
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    total_t = 0.0
+    total_b = 0
+    for B in C5_SIZES:
+        share = float((sizes == B).sum() * B) / float(sizes.sum())
+        count = max(threads, min(int((sizes == B).sum()), (64 << 20) // B))
+        blocks = synth.batch_bytes(count, B)
+        sv = synth.batch_survivors(count, n, k)
+        t, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
+        passes = max(1, int(round(target_s * share / max(t, 1e-9))))
+        for _ in range(passes - 1):
+            t2, _ = O.bench_encode_decode(blocks, n, k, sv, threads, kind)
+            t += t2
+        # weight each class by its share of the batch's bytes
+        rate = count * passes * B / t
+        total_t += share * float(sizes.sum()) / rate
+        total_b += share * float(sizes.sum())
+    return {"value": round(total_b / total_t / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"C5 mix (N={n},K={k}): per size class {list(C5_SIZES)}, nk8_split_block + XXH64 of every "
+                      f"part + nk8_assemble_block from {k} survivors, {threads} pthreads, weighted by the "
+                      f"batch's bytes per class, ~{target_s:.0f} s"}
 
 
 def pmc_traffic(config):

@@ -74,6 +74,20 @@ int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots,
 		    uint64_t block_pitch, uint32_t nstripes, void *d_work,
 		    int32_t *d_status, void *stream);
 
+/* Ragged decode: the layout nkfs_nk8_encode_ragged writes.  Stripe s has
+ * n_slots part slots at d_parts + d_part_off[s] + j*nkfs_part_pitch(
+ * d_block_size[s], k) (d_part_off[s] a multiple of 16) and is rebuilt into
+ * d_blocks + d_block_off[s], d_block_size[s] bytes; max_block_size bounds
+ * every d_block_size[s].  Selection, status and workspace as
+ * nkfs_nk8_decode (crt/nk8.c:446-599 per stripe). */
+int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off,
+			   int n_slots, const uint8_t *d_ids,
+			   const uint8_t *d_avail, int navail, int k,
+			   uint8_t *d_blocks, const uint64_t *d_block_off,
+			   const uint32_t *d_block_size,
+			   uint32_t max_block_size, uint32_t nstripes,
+			   void *d_work, int32_t *d_status, void *stream);
+
 /* nkfs_nk8_decode that also verifies every part it reads against its stored
  * digest (d_expect[s*n_slots + j] = XXH64 of slot j, as produced by
  * nkfs_nk8_encode), the GET-side check of the core's per-block sums

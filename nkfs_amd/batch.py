@@ -104,6 +104,28 @@ def decode(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Te
     return out, status
 
 
+def decode_ragged(parts: torch.Tensor, part_off: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Tensor,
+                  k: int, out: torch.Tensor, block_off: torch.Tensor, block_sizes: torch.Tensor,
+                  max_block_size: int, work: torch.Tensor | None = None, status: torch.Tensor | None = None,
+                  stream=None):
+    """Decode a ragged batch laid out as encode_ragged writes it into out
+    (uint8, stripe s at block_off[s], block_sizes[s] bytes).  Returns status."""
+    for t, dt, nm in ((parts, U8, "parts"), (part_off, torch.int64, "part_off"), (ids, U8, "ids"),
+                      (avail, U8, "avail"), (out, U8, "out"), (block_off, torch.int64, "block_off"),
+                      (block_sizes, torch.int32, "block_sizes")):
+        _need(t, dt, nm)
+    nstripes, navail = avail.shape[0], avail.shape[1]
+    if work is None:
+        work = decode_workspace(nstripes, k, parts.device)
+    if status is None:
+        status = torch.empty(nstripes, dtype=torch.int32, device=parts.device)
+    check(lib().nkfs_nk8_decode_ragged(parts.data_ptr(), part_off.data_ptr(), n_slots, ids.data_ptr(),
+                                       avail.data_ptr(), navail, k, out.data_ptr(), block_off.data_ptr(),
+                                       block_sizes.data_ptr(), max_block_size, nstripes, work.data_ptr(),
+                                       status.data_ptr(), _stream(stream)), "nkfs_nk8_decode_ragged")
+    return status
+
+
 def decode_verify(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: torch.Tensor, k: int,
                   block_size: int, expect: torch.Tensor, out: torch.Tensor | None = None,
                   work: torch.Tensor | None = None, status: torch.Tensor | None = None, stream=None):

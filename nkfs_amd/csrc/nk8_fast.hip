@@ -58,8 +58,9 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     const int gi = lane / LP;
     const int li = lane % LP;
     const int n = g.n;
-    const u32 s = blockIdx.x * G + gi;
-    const bool live = s < g.nstripes;
+    const u32 slot_ = blockIdx.x * G + gi;
+    const bool live = slot_ < g.nstripes;
+    const u32 s = live && g.order ? g.order[slot_] : slot_;
     Stripe v{};
     if (live)
         v = stripe_at(g, s);
@@ -366,8 +367,9 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     // blockIdx.x = group * slices + slice: long stripes are split into row
     // slices on separate waves (decode rows are independent)
     const u32 grp = blockIdx.x / u32(slices), slice = blockIdx.x % u32(slices);
-    const u32 s = grp * G + gi;
-    const bool live = s < g.nstripes;
+    const u32 slot_ = grp * G + gi;
+    const bool live = slot_ < g.nstripes;
+    const u32 s = live && g.order ? g.order[slot_] : slot_;
     inv4[lane] = reinterpret_cast<const u32 *>(inv)[lane];
     // the first LP offered parts and their ids, loaded in parallel
     const u8 *sid = ids + u64(s) * n_slots;
@@ -383,7 +385,18 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     // among them (crt/nk8.c:512-537): request the first step's rows from
     // them now, so the HBM latency hides under the selection, the inverse
     // and the table build; a changed selection reloads below.
-    const u32 B = g.block_size;
+    // geometry of this stripe: uniform, or ragged as nkfs_nk8_encode_ragged
+    // lays it out (part pitch = part size rounded to NKFS_PART_ALIGN)
+    u32 B = g.block_size;
+    u64 ppitch = g.part_pitch;
+    const u8 *pbase = g.parts + u64(s) * n_slots * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+    if (g.block_sizes) {
+        B = live ? g.block_sizes[s] : 0u;
+        ppitch = (u64(part_size_of(B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
+        pbase = live ? g.parts + g.part_off[s] : g.parts;
+        out = live ? const_cast<u8 *>(g.blocks) + g.block_off[s] : out;
+    }
     const u32 ps = part_size_of(B, K);
     const u32 steps = (ps + R - 1) / R, per = VERIFY ? steps : (steps + slices - 1) / slices;
     const u32 rend = VERIFY ? ps : min(ps, (slice + 1) * per * R);
@@ -393,7 +406,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
     for (int c = 0; c < K; ++c) {
         spec[c] = (c < navail && c < LP) ? cand_slot[gi][c] : 0;
-        src[c] = g.parts + (u64(s) * n_slots + spec[c]) * g.part_pitch;
+        src[c] = pbase + spec[c] * ppitch;
     }
     u32 pv[K][4];
     auto load_step = [&](u32 r0) {
@@ -503,12 +516,11 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
     for (int c = 0; c < K; ++c) {
         respec |= slot[gi][c] != spec[c];
-        src[c] = g.parts + (u64(s) * n_slots + slot[gi][c]) * g.part_pitch;
+        src[c] = pbase + slot[gi][c] * ppitch;
     }
     if (respec && rfirst < rend)
         load_step(rfirst);
-    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | (g.block_sizes ? 0 : g.block_pitch)) & 15) == 0;
     auto rebuild = [&](u32 (&o)[4 * K]) {
         // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
         // bytes are packed into K output dwords with v_perm (<= 2 per dword)

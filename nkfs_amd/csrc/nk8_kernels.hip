@@ -322,21 +322,19 @@ __global__ __launch_bounds__(256) void k_decode_generic(nkfs_geom g, int n_slots
     if (status && status[s])
         return;
     const int k = g.k;
-    const u32 B = g.block_size;
-    const u32 ps = part_size_of(B, k);
+    const StripeView v = stripe_view(g, s);  // g.n = n_slots; blocks = the output
     const u32 j = blockIdx.y * blockDim.x + threadIdx.x;
-    if (j >= ps)
+    if (j >= v.ps)
         return;
     const u8 *wk = work + u64(s) * u64(k + k * k);
-    const u8 *sparts = g.parts + u64(s) * u64(n_slots) * g.part_pitch;
-    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+    u8 *out = const_cast<u8 *>(v.blk);
     const u64 row = u64(j) * k;
     for (int m = 0; m < k; ++m) {
-        if (row + m >= B)
+        if (row + m >= v.B)
             break;
         u8 acc = 0;
         for (int c = 0; c < k; ++c) {
-            const u8 pv = sparts[u64(wk[c]) * g.part_pitch + j];
+            const u8 pv = v.parts[u64(wk[c]) * v.pitch + j];
             acc ^= gf_mul(L, pv, wk[k + c * k + m]);
         }
         out[row + m] = acc;
@@ -354,7 +352,8 @@ __global__ __launch_bounds__(64) void k_verify_generic(nkfs_geom g, int n_slots,
     if (status && status[s] == -EINVAL)
         return;
     const u8 *wk = work + u64(s) * u64(k + k * k);
-    const u32 ps = part_size_of(g.block_size, k);
+    const StripeView v = stripe_view(g, s);
+    const u32 ps = v.ps;
     const u32 nst = ps >> 5;
     if (threadIdx.x == 0 && badmask)
         badmask[s] = 0;
@@ -363,7 +362,7 @@ __global__ __launch_bounds__(64) void k_verify_generic(nkfs_geom g, int n_slots,
         const int c = c0 + int(threadIdx.x >> 2), a = int(threadIdx.x & 3);
         const bool live = c < k;
         const u8 sl = live ? wk[c] : 0;
-        const u8 *p = g.parts + (u64(s) * n_slots + sl) * g.part_pitch;
+        const u8 *p = v.parts + u64(sl) * v.pitch;
         u64 acc = xxh_acc_init(a, 0);
         const u64 *w = reinterpret_cast<const u64 *>(p) + a;
         for (u32 r = 0; live && r < nst; ++r)
@@ -382,6 +381,48 @@ __global__ __launch_bounds__(64) void k_verify_generic(nkfs_geom g, int n_slots,
             }
         }
     }
+}
+
+// ------------------------------------------------- ragged batch order
+//
+// Ragged batches (mixed stripe sizes) are processed largest-first, with
+// stripes of similar size side by side: the fused kernels run G stripes of a
+// wave in lock step (a 1 MiB stripe next to a 4 KiB one idles half the wave
+// for the whole stripe) and the longest stripes must not start last (the
+// grid's tail).  One workgroup bucket-sorts the stripes by part size into
+// perm (256 buckets: 8 per octave, largest first).  The order inside a
+// bucket depends on atomics; it changes timing only, never an output.
+__device__ inline u32 size_bucket(u32 B, int k)
+{
+    const u32 ps = part_size_of(B, k);
+    if (!ps)
+        return 255;
+    const u32 lz = 31u - u32(__builtin_clz(ps));
+    const u32 top = lz >= 3 ? (ps >> (lz - 3)) & 7u : (ps << (3 - lz)) & 7u;
+    return 255u - (lz * 8u + top);  // lz <= 28 for 32-bit sizes: no wrap
+}
+
+__global__ __launch_bounds__(1024) void k_order_by_size(const u32 *sizes, u32 count, int k, u32 *perm)
+{
+    __shared__ u32 cnt[256];
+    const u32 t = threadIdx.x;
+    if (t < 256)
+        cnt[t] = 0;
+    __syncthreads();
+    for (u32 i = t; i < count; i += blockDim.x)
+        atomicAdd(&cnt[size_bucket(sizes[i], k)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        u32 run = 0;
+        for (int b = 0; b < 256; ++b) {
+            const u32 c = cnt[b];
+            cnt[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (u32 i = t; i < count; i += blockDim.x)
+        perm[atomicAdd(&cnt[size_bucket(sizes[i], k)], 1u)] = i;
 }
 
 // ---------------------------------------------------------- synthetic
@@ -446,13 +487,38 @@ extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
 }
 
 // ragged batches pass the bound on block sizes in g->block_size
+// Fast-path launch of a ragged batch in size order (k_order_by_size); the
+// permutation lives in stream-ordered scratch, so the call stays capturable.
+// Returns -ENOSYS when the batch is uniform or ordering is switched off.
+template <class F>
+static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
+{
+    if (!g->block_sizes || g->order || getenv("NKFS_NO_ORDER"))
+        return -ENOSYS;
+    u32 *perm = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void **>(&perm), size_t(g->nstripes) * sizeof(u32), st) != hipSuccess)
+        return -ENOSYS;
+    hipLaunchKernelGGL(k_order_by_size, dim3(1), dim3(1024), 0, st, g->block_sizes, g->nstripes, g->k, perm);
+    int rc = launch_ok();
+    nkfs_geom g2 = *g;
+    g2.order = perm;
+    if (!rc)
+        rc = launch(&g2);
+    const hipError_t e = hipFreeAsync(perm, st);
+    return rc ? rc : (e == hipSuccess ? 0 : -EIO);
+}
+
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
                                   void *stream)
 {
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
-    int rc = nkfs_fast_encode(g, ids, digests, gf, st);
+    int rc = -ENOSYS;
+    if (g->n <= 8 && g->k <= 8 && !getenv("NKFS_FORCE_GENERIC"))
+        rc = with_size_order(g, st, [&](const nkfs_geom *go) { return nkfs_fast_encode(go, ids, digests, gf, st); });
+    if (rc == -ENOSYS)
+        rc = nkfs_fast_encode(g, ids, digests, gf, st);
     if (rc != -ENOSYS)
         return rc;
     const u32 ps = max_part_size(g, g->block_size);
@@ -484,7 +550,13 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
-    int rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
+    int rc = -ENOSYS;
+    if (g->k <= 8 && !getenv("NKFS_FORCE_GENERIC"))
+        rc = with_size_order(g, st, [&](const nkfs_geom *go) {
+            return nkfs_fast_decode(go, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
+        });
+    if (rc == -ENOSYS)
+        rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
     if (rc != -ENOSYS)
         return rc;
     hipLaunchKernelGGL(k_decode_prep, dim3(g->nstripes), dim3(64), 0, st, ids, avail, n_slots, navail, g->k,

@@ -26,6 +26,10 @@ struct nkfs_geom {
 	uint32_t nstripes;
 	int n;
 	int k;
+	/* optional processing order (ragged batches): wave slot i handles stripe
+	 * order[i]; NULL = identity.  Only changes which stripes share a wave and
+	 * when they run, never an output. */
+	const uint32_t *order;
 };
 
 /* Launchers: return 0 or a negative errno; `stream` is a hipStream_t. */

@@ -96,7 +96,7 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t
 			err = nkfs_hip_fail("H2D", (int)e);
 			goto out;
 		}
-		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k };
+		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k, NULL };
 		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), s)))
 			goto out;
 		if ((e = hipMemcpyAsync(h_parts + (uint64_t)s0 * n * part_pitch, d_parts, (uint64_t)cnt * n * part_pitch,

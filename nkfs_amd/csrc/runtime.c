@@ -230,7 +230,7 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
-			       nstripes, n, k };
+			       nstripes, n, k, NULL };
 	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
 }
 
@@ -247,7 +247,7 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 	if (!d_blocks || !d_block_off || !d_block_size || !d_ids || !d_parts || !d_part_off)
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
-			       nstripes, n, k };
+			       nstripes, n, k, NULL };
 	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
 }
 
@@ -271,7 +271,7 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
-			       nstripes, n_slots, k };
+			       nstripes, n_slots, k, NULL };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, d_expect,
 				  d_badmask);
 }
@@ -282,6 +282,24 @@ int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, co
 {
 	return decode_common(d_parts, part_pitch, n_slots, d_ids, d_avail, navail, k, block_size, d_blocks,
 			     block_pitch, nstripes, d_work, d_status, NULL, NULL, stream);
+}
+
+int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots, const uint8_t *d_ids,
+			   const uint8_t *d_avail, int navail, int k, uint8_t *d_blocks, const uint64_t *d_block_off,
+			   const uint32_t *d_block_size, uint32_t max_block_size, uint32_t nstripes, void *d_work,
+			   int32_t *d_status, void *stream)
+{
+	if (nkfs_bad_params(max_block_size, navail, k) || n_slots < 1 || n_slots > 255)
+		return -EINVAL;
+	if (!g_ready)
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!d_parts || !d_part_off || !d_ids || !d_avail || !d_blocks || !d_block_off || !d_block_size || !d_work)
+		return -EINVAL;
+	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, (uint8_t *)d_parts, 0,
+			       d_part_off, nstripes, n_slots, k, NULL };
+	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, NULL, NULL);
 }
 
 int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,

@@ -268,6 +268,61 @@ def test_ragged_mixed_batch(L, O):
             assert got[s * n:(s + 1) * n] == want, (s, B)
 
 
+def _ragged_layout(sizes, n, k, block_gap=0, first_off=0):
+    from nkfs_amd import batch
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos, ppos = first_off, 0
+    for s, B in enumerate(sizes):
+        boff[s] = pos
+        poff[s] = ppos
+        pos += int(B) + block_gap
+        ppos += n * batch.part_pitch(int(B), k)
+    return boff, poff, pos, ppos
+
+
+@pytest.mark.parametrize("n,k,gap", [(8, 5, 0), (4, 2, 3), (6, 3, 16), (17, 16, 5)])
+def test_ragged_decode_round_trip(L, O, n, k, gap):
+    """nkfs_nk8_decode_ragged over the layout nkfs_nk8_encode_ragged writes:
+    mixed 4 KiB / 64 KiB / 1 MiB stripes (C5) plus odd sizes, output blocks
+    at unaligned offsets (gap), survivors in seeded random order with an
+    extra slot offered; fast path (k <= 8) and general path (k = 16).  Each
+    stripe must come back bit-exact; one stripe's parts are also checked
+    against the oracle's assemble."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(24)
+    sizes[:6] = (4096, 65536, 1048576, 1, k + 1, 70001)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, gap)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(300 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=300)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff),
+                        None, int(sizes.max()))
+    keep = min(n, k + 1)
+    avail = synth.batch_survivors(len(sizes), n, keep, first=300)
+    out = torch.zeros(pos + 16, dtype=torch.uint8, device="cuda")
+    status = batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(avail), k, out, dev(boff),
+                                 dev(sizes.astype(np.int32)), int(sizes.max()))
+    torch.cuda.synchronize()
+    assert status.abs().sum().item() == 0
+    got = out.cpu().numpy()
+    for s, B in enumerate(sizes):
+        assert np.array_equal(got[boff[s]: boff[s] + B], host[boff[s]: boff[s] + B]), (s, int(B))
+    # gaps between blocks stay untouched (only B bytes per stripe are written)
+    mask = np.ones(pos + 16, bool)
+    for s, B in enumerate(sizes):
+        mask[boff[s]: boff[s] + B] = False
+    assert not got[mask].any()
+    # the oracle rebuilds stripe 2 (1 MiB) from the same device parts
+    s, B = 2, int(sizes[2])
+    pitch = batch.part_pitch(B, k)
+    pn = parts[poff[s]: poff[s] + n * pitch].cpu().numpy().reshape(n, pitch)[:, :batch.part_size(B, k)]
+    sel = list(avail[s])
+    assert np.array_equal(O.decode([pn[j] for j in sel], ids_np[s][sel], k, B), host[boff[s]: boff[s] + B])
+
+
 def test_decode_status_too_few_distinct(L):
     from nkfs_amd import batch
     S, B, n, k = 4, 4096, 4, 2
