@@ -244,11 +244,20 @@ def run_ragged(args, rank, world, device):
         pos += (B + 255) // 256 * 256
         ppos += n * batch.part_pitch(B, k)
     stream = torch.cuda.current_stream(device)
-    # every stripe generated on the device (synth.stripe_bytes of its global
-    # index, cut to its size) and packed back to back
+    # stripes generated on the device, one uniform batch per size class
+    # (stripe ids first + class offset + i), scattered into the packed
+    # buffer in 256-byte rows: a few launches, not one per stripe
     blocks = torch.zeros(pos, dtype=torch.uint8, device=device)
-    for s, B in enumerate(sizes.tolist()):
-        blocks[boff[s]: boff[s] + B].copy_(batch.synth(1, B, first=first + s, device=device)[0, :B])
+    rows = blocks.view(-1, 256)
+    for ci, B in enumerate(C5_SIZES):
+        idx = np.nonzero(sizes == B)[0]
+        if not len(idx):
+            continue
+        data = batch.synth(len(idx), B, first=first + ci * S, device=device)
+        r = (torch.from_numpy(boff[idx] // 256).to(device)[:, None] +
+             torch.arange(B // 256, device=device)[None, :]).reshape(-1)
+        rows[r] = data[:, :B].reshape(-1, 256)
+        del data, r
     ids_np = synth.batch_ids(S, n, first=first)
     ids = torch.from_numpy(ids_np).to(device)
     avail = torch.from_numpy(synth.batch_survivors(S, n, k, first=first)).to(device)
