@@ -344,13 +344,17 @@ __device__ inline u32 gfm(u32 a, u32 b)
 
 }  // namespace
 
-template <int K, int E, int G, bool VERIFY>
+// U = 16-row units per lane per step (one-shot steps for short stripes: a
+// 4 KiB N4K2 stripe is a single step of 2 x 1024 rows at U = 2)
+template <int K, int E, int G, int U, bool VERIFY>
 __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
                                                     int navail, int32_t *status, const u8 *inv, bool nt, int slices,
                                                     const u64 *expect, u64 *badmask)
 {
     constexpr int LP = 64 / G;
-    constexpr int R = 16 * LP;  // rows per stripe per step
+    constexpr int R = 16 * LP;  // rows per unit (one 16-row block per lane)
+    constexpr int RS = R * U;   // rows per stripe per step
+    static_assert(!VERIFY || U == 1, "the verifying form hashes one unit per step");
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
     constexpr int SPX = R + 32;  // verify exchange buffer bytes per part
@@ -398,9 +402,9 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         out = live ? const_cast<u8 *>(g.blocks) + g.block_off[s] : out;
     }
     const u32 ps = part_size_of(B, K);
-    const u32 steps = (ps + R - 1) / R, per = VERIFY ? steps : (steps + slices - 1) / slices;
-    const u32 rend = VERIFY ? ps : min(ps, (slice + 1) * per * R);
-    const u32 rfirst = (VERIFY ? 0u : slice * per * R) + 16 * li;
+    const u32 steps = (ps + RS - 1) / RS, per = VERIFY ? steps : (steps + slices - 1) / slices;
+    const u32 rend = VERIFY ? ps : min(ps, (slice + 1) * per * RS);
+    const u32 rfirst = (VERIFY ? 0u : slice * per * RS) + 16 * li;
     u8 spec[K];
     const u8 *src[K];
 #pragma unroll
@@ -408,24 +412,53 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
         spec[c] = (c < navail && c < LP) ? cand_slot[gi][c] : 0;
         src[c] = pbase + spec[c] * ppitch;
     }
-    u32 pv[K][4];
-    auto load_step = [&](u32 r0) {
+    u32 pv[U][K][4];
+    auto load_step = [&](u32 r0) {  // caller checks r0 < rend; later units check themselves
 #pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
-            pv[c][0] = t.x;
-            pv[c][1] = t.y;
-            pv[c][2] = t.z;
-            pv[c][3] = t.w;
+        for (int u = 0; u < U; ++u) {
+            if (u && r0 + u * R >= rend)
+                continue;
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0 + u * R);  // pitch >= round16(ps)
+                pv[u][c][0] = t.x;
+                pv[u][c][1] = t.y;
+                pv[u][c][2] = t.z;
+                pv[u][c][3] = t.w;
+            }
         }
     };
     if (live && navail >= K && rfirst < rend)
         load_step(rfirst);
 
-    if (li == 0) {
+    // first K distinct ids in offered order (crt/nk8.c:512-537)
+    if (navail <= LP) {
+        // lane-parallel: candidate li is taken when no earlier candidate has
+        // its id and fewer than K earlier candidates were taken
+        const bool cand = live && li < navail;
+        const u8 myid = cand ? cand_id[gi][li] : 0;
+        bool dup = false;
+        for (int j = 0; cand && j < li; ++j)
+            dup |= cand_id[gi][j] == myid;
+        const bool first = cand && !dup;
+        const u64 gmask = LP == 64 ? ~0ull : (((1ull << LP) - 1) << (gi * LP));
+        const u64 taken = u64(__ballot(first)) & gmask;
+        const int rank = __popcll(taken & ((1ull << lane) - 1));
+        if (first && rank < K) {
+            xs[gi][rank] = myid;
+            slot[gi][rank] = cand_slot[gi][li];
+        }
+        if (li == 0) {
+            const int h = min(K, __popcll(taken));
+            have[gi] = h;
+            if (live && status && slice == 0)
+                status[s] = h < K ? -EINVAL : 0;
+            if (live && VERIFY && badmask)
+                badmask[s] = 0;
+        }
+    } else if (li == 0) {
         int h = 0;
         if (live) {
-            // first K distinct ids in offered order (crt/nk8.c:512-537)
             for (int c = 0; c < navail && h < K; ++c) {
                 u8 sl, id;
                 if (c < LP) {
@@ -450,22 +483,24 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                 badmask[s] = 0;
         }
         have[gi] = h;
-        if (h == K) {
-            u32 m[K + 1];
-            m[0] = 1;
+    }
+    __syncthreads();
+    // M(t) = prod_c (t + x_c), by lane 0 of the stripe
+    if (li == 0 && have[gi] == K) {
+        u32 m[K + 1];
+        m[0] = 1;
 #pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const u32 x = xs[gi][c];
-                m[c + 1] = m[c];
+        for (int c = 0; c < K; ++c) {
+            const u32 x = xs[gi][c];
+            m[c + 1] = m[c];
 #pragma unroll
-                for (int i = c; i >= 1; --i)
-                    m[i] = m[i - 1] ^ gfm(x, m[i]);
-                m[0] = gfm(x, m[0]);
-            }
-#pragma unroll
-            for (int i = 0; i <= K; ++i)
-                M[gi][i] = u8(m[i]);
+            for (int i = c; i >= 1; --i)
+                m[i] = m[i - 1] ^ gfm(x, m[i]);
+            m[0] = gfm(x, m[0]);
         }
+#pragma unroll
+        for (int i = 0; i <= K; ++i)
+            M[gi][i] = u8(m[i]);
     }
     __syncthreads();
     const bool ok = have[gi] == K;
@@ -521,9 +556,13 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     if (respec && rfirst < rend)
         load_step(rfirst);
     const bool aligned = ((reinterpret_cast<uintptr_t>(out) | (g.block_sizes ? 0 : g.block_pitch)) & 15) == 0;
-    auto rebuild = [&](u32 (&o)[4 * K]) {
+    auto rebuild = [&](u32 (&o)[4 * K], int u) {
         // 16 rows in four groups of 4: lookups, XOR, then the group's 4*K
-        // bytes are packed into K output dwords with v_perm (<= 2 per dword)
+        // bytes are packed into K output dwords with v_perm (<= 2 per dword).
+        // Each group's table addresses depend (opaquely, tdep == 0) on the
+        // previous group's result: hoisting all 16*K lookups ahead would hold
+        // them in VGPRs at once (205 VGPRs at K = 5, 2 waves per SIMD)
+        u32 tdep = 0;
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             u32 row[4 * W];
@@ -535,8 +574,8 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
                     row[rr * W + w] = 0;
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    const u32 byte = (pv[c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                    const u8 *e = mytbl + c * TB + byte * E;
+                    const u32 byte = (pv[u][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                    const u8 *e = mytbl + tdep + c * TB + byte * E;
                     if constexpr (E == 8) {
                         const uint2 t = *reinterpret_cast<const uint2 *>(e);
                         row[rr * W] ^= t.x;
@@ -549,6 +588,8 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
             for (int q = 0; q < K; ++q)
                 o[gq * K + q] = pack_dword<K, W>(row, q);
+            if constexpr (K * W > 8)
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(o[gq * K]));
         }
     };
     auto emit = [&](const u32 (&o)[4 * K], u32 r0) {
@@ -568,12 +609,18 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     };
 
     if constexpr (!VERIFY) {
-        for (u32 r0 = rfirst; r0 < rend; r0 += R) {
-            u32 o[4 * K];
-            rebuild(o);
-            if (r0 + R < rend)
-                load_step(r0 + R);  // prefetch the next step under this one's stores
-            emit(o, r0);
+        for (u32 r0 = rfirst; r0 < rend; r0 += RS) {
+            u32 o[U][4 * K];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (!u || r0 + u * R < rend)
+                    rebuild(o[u], u);
+            if (r0 + RS < rend)
+                load_step(r0 + RS);  // prefetch the next step under this one's stores
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (!u || r0 + u * R < rend)
+                    emit(o[u], r0 + u * R);
         }
     } else {
         // Integrity-checked decode: the k parts read for the rebuild are also
@@ -593,7 +640,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
             const bool act = t < steps && r0 < ps;
             u32 o[4 * K];
             if (act)
-                rebuild(o);
+                rebuild(o, 0);
 #pragma unroll
             for (int r = 0; r < RPC; ++r) {
                 const u64 nxt = xxh_round(acc, hw[r]);
@@ -603,7 +650,7 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
 #pragma unroll
                 for (int c = 0; c < K; ++c)
                     *reinterpret_cast<uint4 *>(xbuf + (gi * K + c) * SPX + 16 * li) =
-                        make_uint4(pv[c][0], pv[c][1], pv[c][2], pv[c][3]);
+                        make_uint4(pv[0][c][0], pv[0][c][1], pv[0][c][2], pv[0][c][3]);
                 if (r0 + R < ps)
                     load_step(r0 + R);
                 emit(o, r0);
@@ -665,7 +712,13 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4
     // steps; the verifying form hashes each part in order: one slice
     const u32 ps = g->block_size / u32(g->k) + (g->block_size % u32(g->k) ? 1u : 0u);
-    const u32 R = 16u * (64u / u32(G));
+    // two 16-row units per lane per step (one-shot 4 KiB N4K2 stripes, half
+    // the steps of long ones): decode +3 % (C2), +9 % (C3), +6 % (C4) in
+    // one-process A/B (profiles/r01/ab_decode_units.txt); NKFS_DEC_U=1 = old
+    int U = verify ? 1 : 2;
+    if (const char *e = getenv("NKFS_DEC_U"))
+        U = atoi(e) == 1 || verify ? 1 : 2;
+    const u32 R = 16u * (64u / u32(G)) * u32(U);
     const u32 steps = (ps + R - 1) / R;
     u32 slices = 1, target = 4096;
     if (const char *e = getenv("NKFS_DEC_WAVES"))  // experiment: wave-count target
@@ -673,14 +726,17 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     while (!verify && groups * slices < target && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
-#define NKFS_DK(KK, EE, GG)                                                                                     \
-    do {                                                                                                        \
-        if (verify)                                                                                             \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, true>), grid, dim3(64), 0, st, *g, n_slots, ids, avail, \
-                               navail, status, t->inv, nt, int(slices), expect, badmask);                       \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, false>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                \
+#define NKFS_DK(KK, EE, GG)                                                                                       \
+    do {                                                                                                          \
+        if (verify)                                                                                               \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, true>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
+                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
+        else if (U == 2)                                                                                          \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
+                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
+                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
     } while (0)
     switch (g->k) {
     case 2: NKFS_DK(2, 4, 1); break;
