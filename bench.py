@@ -415,12 +415,12 @@ def pcie_rate(batch, blocks_np, S, B, n, k, ids, avail, device, stream):
     on two streams.  User GiB/s; DESIGN.md records it (never the headline)."""
     import torch
     host_in = torch.from_numpy(blocks_np).pin_memory()
-    ids_h = ids.cpu()
-    batch.encode_host(host_in, B, n, k, ids_h)  # warm-up (allocations, pinning)
-    reps = 3
+    ids_h = ids.cpu().pin_memory()
+    out = batch.encode_host(host_in, B, n, k, ids_h)  # warm-up: pinned outputs, pooled streams/scratch
+    reps = 5
     t0 = time.perf_counter()
     for _ in range(reps):
-        parts, dig = batch.encode_host(host_in, B, n, k, ids_h)
+        batch.encode_host(host_in, B, n, k, ids_h, out=out)
     t1 = time.perf_counter()
     return round(S * B * reps / (t1 - t0) / 2**30, 3)
 

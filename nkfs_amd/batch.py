@@ -153,10 +153,12 @@ def decode_verify(parts: torch.Tensor, n_slots: int, ids: torch.Tensor, avail: t
     return out, status, bad
 
 
-def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int = 0, digests: bool = True):
+def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int = 0, digests: bool = True,
+                out=None):
     """Host-memory encode (+XXH64): blocks uint8 [nstripes, pitch] and ids
     uint8 [nstripes, n] as numpy arrays or CPU tensors (pinned is fastest);
-    streams through the GPU in sub-batches (nkfs_nk8_encode_host).
+    streams through the GPU in sub-batches (nkfs_nk8_encode_host).  out =
+    (parts, digests|None) reuses caller buffers (pinned: no per-call pin).
     Returns (parts [nstripes*n, part_pitch] CPU tensor, digests or None)."""
     bt = torch.as_tensor(blocks)
     it = torch.as_tensor(ids)
@@ -164,8 +166,15 @@ def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int =
         raise ValueError("blocks/ids: contiguous uint8 host arrays")
     nstripes = bt.shape[0]
     pitch = part_pitch(block_size, k)
-    parts = torch.empty((nstripes * n, pitch), dtype=U8, pin_memory=torch.cuda.is_available())
-    dig = torch.empty(nstripes * n, dtype=torch.int64, pin_memory=torch.cuda.is_available()) if digests else None
+    if out is not None:
+        parts, dig = out
+        if parts.shape != (nstripes * n, pitch) or parts.dtype != U8 or parts.is_cuda or not parts.is_contiguous():
+            raise ValueError("out parts: contiguous uint8 host tensor [nstripes*n, part_pitch]")
+        if dig is not None and (dig.numel() != nstripes * n or dig.dtype != torch.int64 or dig.is_cuda):
+            raise ValueError("out digests: int64 host tensor [nstripes*n]")
+    else:
+        parts = torch.empty((nstripes * n, pitch), dtype=U8, pin_memory=torch.cuda.is_available())
+        dig = torch.empty(nstripes * n, dtype=torch.int64, pin_memory=torch.cuda.is_available()) if digests else None
     check(lib().nkfs_nk8_encode_host(bt.data_ptr(), bt.stride(0) if bt.dim() > 1 else block_size, block_size,
                                      nstripes, n, k, it.contiguous().data_ptr(), parts.data_ptr(), pitch,
                                      _ptr(dig), chunk_bytes), "nkfs_nk8_encode_host")

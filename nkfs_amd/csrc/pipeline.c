@@ -36,7 +36,11 @@ static int pin(const void *p, size_t bytes, int *registered)
 	return 0;
 }
 
-#define NSTREAM 2
+/* Three sub-batches in flight (H2D of one, kernels of another, D2H of a
+ * third); each rides a pooled context (its stream and growable device
+ * scratch are reused across calls, so a call creates no streams and
+ * allocates no device memory once warm). */
+#define NSTREAM 3
 
 int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
 			 int n, int k, const uint8_t *h_ids, uint8_t *h_parts, uint64_t part_pitch,
@@ -63,30 +67,33 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t
 	const uint64_t in_bytes = (uint64_t)(nstripes - 1) * bp + block_size;
 	const uint64_t parts_bytes = (uint64_t)nstripes * n * part_pitch;
 	int reg[4] = {0, 0, 0, 0}, err;
+	struct nkfs_ctx *cx[NSTREAM] = {0};
 	if ((err = pin(h_blocks, in_bytes, &reg[0])) || (err = pin(h_ids, (size_t)nstripes * n, &reg[1])) ||
 	    (err = pin(h_parts, parts_bytes, &reg[2])) ||
 	    (err = pin(h_digests, h_digests ? (size_t)nstripes * n * 8 : 0, &reg[3])))
 		goto unpin;
 
-	/* per stream: blocks | parts | ids | digests (device) */
+	/* per context: blocks | parts | ids | digests (device) */
 	const uint64_t dblk = (uint64_t)per * bp;
 	const uint64_t dparts = (uint64_t)per * n * part_pitch;
 	const uint64_t dids = ((uint64_t)per * n + 255) & ~255ull;
 	const uint64_t ddig = (uint64_t)per * n * 8;
 	const uint64_t slot = ((dblk + 255) & ~255ull) + dparts + dids + ddig;
-	hipStream_t st[NSTREAM] = {0};
-	uint8_t *dev = NULL;
-	hipError_t e = hipMalloc((void **)&dev, slot * NSTREAM);
-	for (int i = 0; e == hipSuccess && i < NSTREAM; i++)
-		e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
-	if (e != hipSuccess) {
-		err = nkfs_hip_fail("pipeline setup", (int)e);
-		goto out;
+	void *dev[NSTREAM];
+	hipError_t e = hipSuccess;
+	for (int i = 0; i < NSTREAM; i++) {
+		cx[i] = nkfs_ctx_get();
+		if (!cx[i]) {
+			err = -ENOMEM;
+			goto out;
+		}
+		if ((err = nkfs_ctx_dev(cx[i], slot, &dev[i])))
+			goto out;
 	}
 	for (uint32_t s0 = 0, it = 0; s0 < nstripes; s0 += per, it++) {
 		const uint32_t cnt = nstripes - s0 < per ? nstripes - s0 : per;
-		hipStream_t s = st[it % NSTREAM];
-		uint8_t *d = dev + slot * (it % NSTREAM);
+		hipStream_t s = cx[it % NSTREAM]->stream;
+		uint8_t *d = (uint8_t *)dev[it % NSTREAM];
 		uint8_t *d_blk = d, *d_parts = d + ((dblk + 255) & ~255ull);
 		uint8_t *d_ids = d_parts + dparts;
 		uint64_t *d_dig = (uint64_t *)(d_ids + dids);
@@ -107,19 +114,14 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t
 			goto out;
 		}
 	}
-	for (int i = 0; i < NSTREAM; i++)
-		if ((e = hipStreamSynchronize(st[i])) != hipSuccess) {
-			err = nkfs_hip_fail("pipeline sync", (int)e);
-			goto out;
-		}
 	err = 0;
 out:
 	for (int i = 0; i < NSTREAM; i++)
-		if (st[i]) {
-			hipStreamSynchronize(st[i]);
-			hipStreamDestroy(st[i]);
+		if (cx[i]) {
+			if ((e = hipStreamSynchronize(cx[i]->stream)) != hipSuccess && !err)
+				err = nkfs_hip_fail("pipeline sync", (int)e);
+			nkfs_ctx_put(cx[i]);
 		}
-	hipFree(dev);
 unpin:
 	if (reg[0])
 		hipHostUnregister((void *)h_blocks);
