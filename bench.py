@@ -109,8 +109,10 @@ def main():
     args = parse()
     import torch
 
+    # the rank's GPU is selected before the process group exists, so RCCL's
+    # communicator binds to it (one process per GPU)
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     rank, world, local = dist_setup("nccl")
-    torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     os.environ["NKFS_DEVICE"] = str(local)
 
