@@ -486,3 +486,23 @@ def test_decode_verify(L, S, B, n, k):
     assert st[s_unused] == 0 and bm[s_unused] == 0
     assert all(v == 0 for i, v in enumerate(st) if i != s_used)
     assert torch.equal(out[s_unused], blocks[s_unused, :B])
+
+
+@pytest.mark.parametrize("ne,n,k,B", [(4, 4, 2, 4096), (8, 4, 3, 70001), (2, 8, 5, 262144), (4, 8, 6, 1000)])
+def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B):
+    """The experimental warp-specialised encoder (env NKFS_ENC_WS, nk8_ws.hip:
+    encoder waves + one hash wave per workgroup) writes the same parts and
+    digests as the default fused kernel, tails and partial workgroups
+    included."""
+    from nkfs_amd import batch
+    S = 23
+    blocks = batch.synth(S, B, first=77)
+    ids = dev(synth.batch_ids(S, n, first=77))
+    p0, d0 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("NKFS_ENC_WS", str(ne))
+    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps])
+    assert torch.equal(d0, d1)
