@@ -31,7 +31,9 @@
 using namespace nkfs;
 using namespace nkfs::dev;
 
-template <int K, int E, int NE>
+// SB: single-buffered exchange (the hash wave copies its words to registers
+// between two barriers per chunk) -- half the LDS, so more workgroups per CU
+template <int K, int E, int NE, bool SB>
 __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
     constexpr int S = 16 / E;       // stripes per workgroup: 4 accumulators x E parts x S = 64 chains
@@ -43,7 +45,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     constexpr int W = E / 4;        // dwords per packed entry
     constexpr int RPC = CR / 32;    // XXH64 rounds per chain per chunk
     __shared__ __attribute__((aligned(16))) u8 tbl[S * (K - 1) * TB];
-    __shared__ __attribute__((aligned(16))) u8 xbuf[2][S * E * SP];
+    __shared__ __attribute__((aligned(16))) u8 xbuf[SB ? 1 : 2][S * E * SP];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool hasher = wave == NE;
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
                 }
                 if (r0 + CR < v.ps)
                     load_task(r0 + CR);  // next chunk's rows in flight under this chunk's stores
-                u8 *xb = xbuf[c & 1] + gs * E * SP + sub * 1024 + 16 * lane;
+                u8 *xb = xbuf[SB ? 0 : (c & 1)] + gs * E * SP + sub * 1024 + 16 * lane;
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
                     if (i < n) {
@@ -185,6 +187,8 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
                 }
             }
             __syncthreads();
+            if constexpr (SB)
+                __syncthreads();  // the hash wave has copied the chunk
         }
         return;
     }
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     u64 acc = xxh_acc_init(ha, 0);
     const int xoff = (hs * E + hi) * SP + 8 * ha;
     auto fold = [&](u32 c) {
-        const u8 *src = xbuf[c & 1] + xoff;
+        const u8 *src = xbuf[SB ? 0 : (c & 1)] + xoff;
         const int left = int(nst) - int(c * RPC);
         if (left >= RPC) {
 #pragma unroll 8
@@ -216,13 +220,42 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
         }
     };
     __syncthreads();  // tables built (the encoders' first barrier)
-    for (u32 c = 0; c < nch; ++c) {
-        if (hlane && c >= 1 && c - 1 < own)
-            fold(c - 1);
-        __syncthreads();
+    if constexpr (SB) {
+        static_assert(RPC <= 32, "hash words staged in registers");
+        for (u32 c = 0; c < nch; ++c) {
+            __syncthreads();  // chunk c is in the exchange
+            u64 hw[RPC];
+            int hv = 0;
+            if (hlane && c < own) {
+                const u8 *src = xbuf[0] + xoff;
+                const int left = int(nst) - int(c * RPC);
+                hv = left < 0 ? 0 : (left > RPC ? RPC : left);
+#pragma unroll
+                for (int r = 0; r < RPC; ++r)
+                    hw[r] = *reinterpret_cast<const u64 *>(src + 32 * r);
+            }
+            __syncthreads();  // the encoders may overwrite it now
+            if (hv == RPC) {
+#pragma unroll
+                for (int r = 0; r < RPC; ++r)
+                    acc = xxh_round(acc, hw[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < RPC; ++r) {
+                    const u64 nx = xxh_round(acc, hw[r]);
+                    acc = r < hv ? nx : acc;
+                }
+            }
+        }
+    } else {
+        for (u32 c = 0; c < nch; ++c) {
+            if (hlane && c >= 1 && c - 1 < own)
+                fold(c - 1);
+            __syncthreads();
+        }
+        if (hlane && nch >= 1 && nch - 1 < own)
+            fold(nch - 1);
     }
-    if (hlane && nch >= 1 && nch - 1 < own)
-        fold(nch - 1);
 
     const int base = lane & ~3;
     const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
@@ -235,7 +268,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
         if (left) {
             // the tail sits in this stripe's last chunk, untouched since
             const u32 toff = nst * 32 - (own - 1) * CR;
-            const u64 *src = reinterpret_cast<const u64 *>(xbuf[(own - 1) & 1] + (hs * E + hi) * SP + toff);
+            const u64 *src = reinterpret_cast<const u64 *>(xbuf[SB ? 0 : ((own - 1) & 1)] + (hs * E + hi) * SP + toff);
 #pragma unroll
             for (int w = 0; w < 4; ++w)
                 tw[w] = src[w];
@@ -244,7 +277,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     }
 }
 
-template <int E, int NE>
+template <int E, int NE, bool SB>
 static int launch_ws(int k, hipStream_t st, const nkfs_geom &g, const uint8_t *ids, uint64_t *dig, bool nt)
 {
     constexpr int S = 16 / E;
@@ -252,7 +285,7 @@ static int launch_ws(int k, hipStream_t st, const nkfs_geom &g, const uint8_t *i
     switch (k) {
 #define NKFS_K(KK)                                                                         \
     case KK:                                                                               \
-        hipLaunchKernelGGL((k_encode_ws<KK, E, NE>), grid, block, 0, st, g, ids, dig, nt); \
+        hipLaunchKernelGGL((k_encode_ws<KK, E, NE, SB>), grid, block, 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -275,11 +308,17 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
 {
     if (g->n > 8 || g->k > 8 || !digests)
         return -ENOSYS;
+    const char *e = getenv("NKFS_ENC_WS_SB");  // single-buffered exchange (n <= 4: ne = 4; n <= 8: ne = 2)
+    const bool sb = e && atoi(e);
     int rc;
     if (g->n <= 4)
-        rc = ne == 8 ? launch_ws<4, 8>(g->k, st, *g, ids, digests, nt) : launch_ws<4, 4>(g->k, st, *g, ids, digests, nt);
+        rc = sb ? launch_ws<4, 4, true>(g->k, st, *g, ids, digests, nt)
+                : (ne == 8 ? launch_ws<4, 8, false>(g->k, st, *g, ids, digests, nt)
+                           : launch_ws<4, 4, false>(g->k, st, *g, ids, digests, nt));
     else
-        rc = ne == 4 ? launch_ws<8, 4>(g->k, st, *g, ids, digests, nt) : launch_ws<8, 2>(g->k, st, *g, ids, digests, nt);
+        rc = sb ? launch_ws<8, 2, true>(g->k, st, *g, ids, digests, nt)
+                : (ne == 4 ? launch_ws<8, 4, false>(g->k, st, *g, ids, digests, nt)
+                           : launch_ws<8, 2, false>(g->k, st, *g, ids, digests, nt));
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -488,8 +488,9 @@ def test_decode_verify(L, S, B, n, k):
     assert torch.equal(out[s_unused], blocks[s_unused, :B])
 
 
-@pytest.mark.parametrize("ne,n,k,B", [(4, 4, 2, 4096), (8, 4, 3, 70001), (2, 8, 5, 262144), (4, 8, 6, 1000)])
-def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B):
+@pytest.mark.parametrize("ne,n,k,B,sb", [(4, 4, 2, 4096, "0"), (8, 4, 3, 70001, "0"), (2, 8, 5, 262144, "0"),
+                                         (4, 8, 6, 1000, "0"), (4, 4, 2, 70001, "1"), (2, 8, 5, 262144, "1")])
+def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
     """The experimental warp-specialised encoder (env NKFS_ENC_WS, nk8_ws.hip:
     encoder waves + one hash wave per workgroup) writes the same parts and
     digests as the default fused kernel, tails and partial workgroups
@@ -501,6 +502,7 @@ def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B):
     p0, d0 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     monkeypatch.setenv("NKFS_ENC_WS", str(ne))
+    monkeypatch.setenv("NKFS_ENC_WS_SB", sb)
     p1, d1 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
