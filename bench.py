@@ -97,6 +97,36 @@ def gather_digest_xor(local_xor: int, device) -> list[int]:
     return [int(x.item()) & 0xFFFFFFFFFFFFFFFF for x in out]
 
 
+def gather_digests(local, device):
+    """All-gather every rank's per-part digests (int64 [stripes*n], 8n bytes
+    per stripe: SURVEY.md §8(e) collective (2)) -> list of CPU tensors, one
+    per rank."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [local.cpu()]
+    out = [torch.empty_like(local) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, local.to(device))
+    return [t.cpu() for t in out]
+
+
+def check_rank_digests(gathered, per_rank, B, n, k, samples=8):
+    """Rank 0's cross-rank check: for a sample of every rank's stripes, the
+    oracle's parts and XXH64 of the regenerated input (synth is a pure
+    function of the global stripe index) equal the digests that rank
+    produced.  Returns the number of ranks verified, or -1 on a mismatch."""
+    from nkfs_amd import synth
+    from oracle import oracle as O
+    for r, dig in enumerate(gathered):
+        d = [int(x) & 0xFFFFFFFFFFFFFFFF for x in dig.tolist()]
+        for s in range(0, per_rank, max(1, per_rank // samples)):
+            g = r * per_rank + s
+            want = [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
+            if d[s * n:(s + 1) * n] != want:
+                return -1
+    return len(gathered)
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
@@ -178,6 +208,9 @@ def main():
     for d in dig:
         dx ^= d
     gathered = gather_digest_xor(dx, device)
+    all_dig = gather_digests(digests, device)
+    ranks_ok = check_rank_digests(all_dig, S, B, n, k) if rank == 0 else None
+    ok &= ranks_ok != -1
     enc_bytes = S * (B + n * ps + 8 * n)
     dec_bytes = S * (k * ps + B + k)
 
@@ -212,6 +245,7 @@ def main():
         "decode": {"achieved_GBps": round(dec_bytes / dec_s / 1e9, 1), "us_per_launch": round(dec_s * 1e6, 2),
                    "bytes_per_launch": dec_bytes},
         "verified": ok,
+        "verified_ranks": ranks_ok,
         "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -28,8 +28,25 @@ def _worker(rank, world, port, q):
     first, count = bench.stripe_range(r, 65536)
     t = bench.reduce_max(1.0 + r, dev)
     xs = bench.gather_digest_xor((0xF000_0000_0000_0000 | r), dev)
+    # per-part digests of this rank's stripes, as the device would produce
+    # them (oracle), all-gathered and checked by rank 0 against regenerated
+    # inputs of every rank
+    from nkfs_amd import synth
+    from oracle import oracle as O
+    per, B, n, k = 4, 300, 4, 2
+    mine = []
+    for s in range(per):
+        g = r * per + s
+        mine += [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
+    local = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in mine], dtype=torch.int64)
+    gathered = bench.gather_digests(local, dev)
+    ok = bench.check_rank_digests(gathered, per, B, n, k, samples=per) if r == 0 else None
+    if r == 1:  # a wrong digest on rank 1 is caught by rank 0
+        local[5] += 1
+    bad = bench.gather_digests(local, dev)
+    nok = bench.check_rank_digests(bad, per, B, n, k, samples=per) if r == 0 else None
     bench.barrier()
-    q.put((r, w, local, first, count, t, xs))
+    q.put((r, w, local.numel(), first, count, t, xs, ok, nok))
     dist.destroy_process_group()
 
 
@@ -45,8 +62,10 @@ def test_two_rank_gloo():
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    for r, (rank, world, local, first, count, t, xs) in enumerate(res):
-        assert (rank, world, local) == (r, 2, r)
+    for r, (rank, world, nd, first, count, t, xs, ok, nok) in enumerate(res):
+        assert (rank, world, nd) == (r, 2, 16)
+        if r == 0:
+            assert ok == 2 and nok == -1
         assert (first, count) == (r * 65536, 65536)  # disjoint stripe ranges, fixed per-GPU work
         assert t == 2.0                              # max over ranks
         assert xs == [0xF000_0000_0000_0000, 0xF000_0000_0000_0001]
