@@ -42,16 +42,25 @@ using namespace nkfs::dev;
 // P = chunks of rows in flight per lane (prefetch depth, rotating register
 // slots): grids with few waves per SIMD (big stripes) cannot hide HBM
 // latency behind other waves, so each wave keeps more of its own loads out.
-template <int K, int E, int P, bool HASH>
+//
+// NIB: nibble tables.  Multiplication by a constant is GF(2)-linear, so
+// T_m[x] = L_m[x & 15] ^ H_m[x >> 4] with 16-entry tables L_m[v] = T_m[v],
+// H_m[v] = T_m[v << 4]: two lookups per byte instead of one, but a
+// half-table's 16 entries sit in distinct LDS banks (same entry =
+// broadcast), so lookups never conflict, and the tables take 32 entries per
+// m instead of 256.  Stripes that share a 32-lane LDS group are offset by
+// half a bank row so their halves use disjoint banks.
+template <int K, int E, int P, bool HASH, bool NIB>
 __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
     constexpr int G = E == 4 ? 4 : 2;   // stripes per wave
     constexpr int LP = 64 / G;          // lanes per stripe
     constexpr int R = 16 * LP;          // rows per stripe per chunk
     constexpr int SP = R + 32;          // LDS bytes per part in the exchange buffer (bank spread)
-    constexpr int TB = 256 * E;         // bytes per packed table
+    constexpr int TB = (NIB ? 32 : 256) * E;  // bytes per packed table (per m)
+    constexpr int TS = (K - 1) * TB + (NIB ? 16 * E : 0);  // bytes per stripe (+ bank offset room)
     constexpr int W = E / 4;            // dwords per packed entry
-    __shared__ __attribute__((aligned(16))) u8 tbl[G * (K - 1) * TB];
+    __shared__ __attribute__((aligned(16))) u8 tbl[G * TS];
     __shared__ __attribute__((aligned(16))) u8 xbuf[G * E * SP];
 
     const int lane = threadIdx.x;
@@ -119,12 +128,37 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
         idw[w] = x;
         coef[w] = x;
     }
-    u8 *mytbl = tbl + gi * (K - 1) * TB;
+    u8 *mytbl = tbl + gi * TS + (NIB ? (gi & 1) * 16 * E : 0);
 #pragma unroll
     for (int m = 1; m < K; ++m) {
         u32 basis[8][W];
         make_basis<W>(basis, coef);
-        build_table<W, LP>(mytbl + (m - 1) * TB, basis, li);
+        if constexpr (NIB) {
+            // entry e: half h = e >> 4 (low / high nibble), value v = e & 15
+#pragma unroll
+            for (int e0 = 0; e0 < 32; e0 += LP) {
+                const int e = e0 + li;
+                if (e < 32) {
+                    const int v = e & 15, h = e >> 4;
+                    u32 val[W];
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        u32 x = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            x ^= basis[4 * h + b][w] & (0u - u32((v >> b) & 1));
+                        val[w] = x;
+                    }
+                    u8 *dst = mytbl + (m - 1) * TB + e * E;
+                    if constexpr (W == 2)
+                        *reinterpret_cast<uint2 *>(dst) = make_uint2(val[0], val[1]);
+                    else
+                        *reinterpret_cast<u32 *>(dst) = val[0];
+                }
+            }
+        } else {
+            build_table<W, LP>(mytbl + (m - 1) * TB, basis, li);
+        }
 #pragma unroll
         for (int w = 0; w < W; ++w)
             coef[w] = gf_mul_packed(coef[w], idw[w]);
@@ -153,13 +187,26 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
                 for (int m = 1; m < K; ++m) {
                     const int p = p0 + m;
                     const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
-                    const u8 *e = mytbl + (m - 1) * TB + byte * E;
-                    if constexpr (E == 8) {
-                        const uint2 t = *reinterpret_cast<const uint2 *>(e);
-                        row[r][0] ^= t.x;
-                        row[r][1] ^= t.y;
+                    if constexpr (NIB) {
+                        const u8 *e0 = mytbl + (m - 1) * TB + (byte & 15u) * E;
+                        const u8 *e1 = mytbl + (m - 1) * TB + (16u + (byte >> 4)) * E;
+                        if constexpr (E == 8) {
+                            const uint2 t0 = *reinterpret_cast<const uint2 *>(e0);
+                            const uint2 t1 = *reinterpret_cast<const uint2 *>(e1);
+                            row[r][0] ^= t0.x ^ t1.x;
+                            row[r][1] ^= t0.y ^ t1.y;
+                        } else {
+                            row[r][0] ^= *reinterpret_cast<const u32 *>(e0) ^ *reinterpret_cast<const u32 *>(e1);
+                        }
                     } else {
-                        row[r][0] ^= *reinterpret_cast<const u32 *>(e);
+                        const u8 *e = mytbl + (m - 1) * TB + byte * E;
+                        if constexpr (E == 8) {
+                            const uint2 t = *reinterpret_cast<const uint2 *>(e);
+                            row[r][0] ^= t.x;
+                            row[r][1] ^= t.y;
+                        } else {
+                            row[r][0] ^= *reinterpret_cast<const u32 *>(e);
+                        }
                     }
                 }
             }
@@ -252,7 +299,7 @@ static bool store_nt()
     return e ? atoi(e) != 0 : false;
 }
 
-template <int E, int P, bool HASH>
+template <int E, int P, bool HASH, bool NIB>
 static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
 {
     constexpr int G = E == 4 ? 4 : 2;
@@ -260,7 +307,7 @@ static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
     switch (k) {
 #define NKFS_K(KK)                                                                                  \
     case KK:                                                                                        \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH>), grid, dim3(64), 0, st, g, ids, dig, nt); \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH, NIB>), grid, dim3(64), 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -276,13 +323,10 @@ static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
 }
 
 template <int E, bool HASH>
-static int launch_p(int P, int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
+static int launch_p(int P, bool nib, int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
 {
-    switch (P) {
-    case 1: return launch_k<E, 1, HASH>(k, st, g, ids, dig, nt);
-    case 2: return launch_k<E, 2, HASH>(k, st, g, ids, dig, nt);
-    default: return launch_k<E, 3, HASH>(k, st, g, ids, dig, nt);
-    }
+    (void)P;  // depths 2-3 measured slower; only P = 1 is instantiated
+    return nib ? launch_k<E, 1, HASH, true>(k, st, g, ids, dig, nt) : launch_k<E, 1, HASH, false>(k, st, g, ids, dig, nt);
 }
 
 extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int ne, bool nt,
@@ -305,10 +349,19 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     int P = 1;
     if (const char *e = getenv("NKFS_ENC_PREFETCH"))  // experiment: prefetch depth
         P = atoi(e);
-    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, g->k, st, *g, ids, digests, nt)
-                                     : launch_p<4, false>(P, g->k, st, *g, ids, digests, nt))
-                          : (digests ? launch_p<8, true>(P, g->k, st, *g, ids, digests, nt)
-                                     : launch_p<8, false>(P, g->k, st, *g, ids, digests, nt));
+    // Nibble tables free LDS (N8K5: 25 -> 11 KB per wave, the occupancy
+    // limit) at twice the lookups: a win where the grid offers more waves
+    // than 25 KB tables let reside (C4 encode +3.2 %), a loss where one wave
+    // per SIMD is issue-bound (C3 -15 %) or LDS never limited (n <= 4: -2 %)
+    // -- profiles/r01/ab_nibble_tables.txt.  NKFS_NIB=0/1 overrides.
+    const u32 waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
+    bool nib = E == 8 && waves >= 2048;
+    if (const char *e = getenv("NKFS_NIB"))
+        nib = atoi(e) != 0;
+    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, st, *g, ids, digests, nt)
+                                     : launch_p<4, false>(P, nib, g->k, st, *g, ids, digests, nt))
+                          : (digests ? launch_p<8, true>(P, nib, g->k, st, *g, ids, digests, nt)
+                                     : launch_p<8, false>(P, nib, g->k, st, *g, ids, digests, nt));
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

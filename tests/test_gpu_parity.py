@@ -508,3 +508,45 @@ def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps])
     assert torch.equal(d0, d1)
+
+
+@pytest.mark.parametrize("n,k,B", [(8, 5, 262144), (8, 8, 4096 * 8 + 5), (6, 3, 70001), (4, 2, 4096), (3, 3, 777),
+                                   (7, 2, 1)])
+def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
+    """Encode with nibble product tables (NKFS_NIB=1; on by default for
+    large n <= 8 grids) equals the 256-entry-table kernel and the oracle,
+    parts and digests, uniform and ragged (size-ordered) batches."""
+    from nkfs_amd import batch
+    S = 20
+    blocks = batch.synth(S, B, first=123)
+    ids_np = synth.batch_ids(S, n, first=123)
+    ids = dev(ids_np)
+    monkeypatch.setenv("NKFS_NIB", "0")
+    p0, d0 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("NKFS_NIB", "1")
+    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    host = blocks.cpu().numpy()
+    for s in (0, S - 1):
+        want = O.encode(host[s, :B], n, k, ids_np[s])
+        assert [u64(x) for x in d1[s * n:(s + 1) * n].cpu().tolist()] == [O.xxh64(p) for p in want]
+    # ragged: mixed sizes through the same tables
+    sizes = np.array([B, 1, 4096, 65536, B // 3 + 1] * 3, np.uint32)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k)
+    hb = np.zeros(pos + 16, np.uint8)
+    for s_, Bs in enumerate(sizes):
+        hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(900 + s_, int(Bs))
+    rid = synth.batch_ids(len(sizes), n, first=900)
+    outs = []
+    for nib in ("0", "1"):
+        monkeypatch.setenv("NKFS_NIB", nib)
+        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+        batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff), dig,
+                            int(sizes.max()))
+        torch.cuda.synchronize()
+        outs.append((parts, dig))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
