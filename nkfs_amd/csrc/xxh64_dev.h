@@ -22,9 +22,21 @@ constexpr uint64_t XP5 = 0x27D4EB2F165667C5ull;
 
 __host__ __device__ inline uint64_t rotl64(uint64_t v, int r) { return (v << r) | (v >> (64 - r)); }
 
+// rotl by 31 as two v_alignbit_b32 on the device (the generic form compiles
+// to a 64-bit shift, a shift and an or)
+__host__ __device__ inline uint64_t rotl64_31(uint64_t v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+    return (uint64_t(__builtin_amdgcn_alignbit(hi, lo, 1)) << 32) | __builtin_amdgcn_alignbit(lo, hi, 1);
+#else
+    return rotl64(v, 31);
+#endif
+}
+
 __host__ __device__ inline uint64_t xxh_round(uint64_t acc, uint64_t w)
 {
-    return rotl64(acc + w * XP2, 31) * XP1;
+    return rotl64_31(acc + w * XP2) * XP1;
 }
 
 // Initial value of accumulator a (0..3) for a seed (xxhash.c:566-577).
