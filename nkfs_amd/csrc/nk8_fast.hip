@@ -343,9 +343,17 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         return -ENOSYS;
     const int E = g->n <= 4 ? 4 : 8;
     const bool nt = store_nt();
-    const char *ws = getenv("NKFS_ENC_WS");  // experiment: warp-specialised kernel, value = encoder waves
-    if (ws && atoi(ws) > 0 && digests)
-        return nkfs_ws_encode(g, ids, digests, atoi(ws), nt, st);
+    // n <= 8 grids of at most one wave per SIMD (few big stripes, e.g. C3:
+    // 2,048 x 1 MiB) are issue-bound in the fused kernel; there the
+    // warp-specialised kernel (4 encoder waves + 1 hash wave per 2 stripes)
+    // measured +3.7 / +3.8 % in two A/Bs (profiles/r01/ab_encode_decode_knobs.txt,
+    // ab_ws_single_buffer.txt).  NKFS_ENC_WS=<encoder waves> forces it, 0 off.
+    const u32 fused_waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
+    int ws_ne = E == 8 && fused_waves <= 1024 ? 4 : 0;
+    if (const char *ws = getenv("NKFS_ENC_WS"))
+        ws_ne = atoi(ws);
+    if (ws_ne > 0 && digests)
+        return nkfs_ws_encode(g, ids, digests, ws_ne, nt, st);
     int P = 1;
     if (const char *e = getenv("NKFS_ENC_PREFETCH"))  // experiment: prefetch depth
         P = atoi(e);
@@ -354,8 +362,7 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // than 25 KB tables let reside (C4 encode +3.2 %), a loss where one wave
     // per SIMD is issue-bound (C3 -15 %) or LDS never limited (n <= 4: -2 %)
     // -- profiles/r01/ab_nibble_tables.txt.  NKFS_NIB=0/1 overrides.
-    const u32 waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
-    bool nib = E == 8 && waves >= 2048;
+    bool nib = E == 8 && fused_waves >= 2048;
     if (const char *e = getenv("NKFS_NIB"))
         nib = atoi(e) != 0;
     const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, st, *g, ids, digests, nt)

@@ -491,14 +491,15 @@ def test_decode_verify(L, S, B, n, k):
 @pytest.mark.parametrize("ne,n,k,B,sb", [(4, 4, 2, 4096, "0"), (8, 4, 3, 70001, "0"), (2, 8, 5, 262144, "0"),
                                          (4, 8, 6, 1000, "0"), (4, 4, 2, 70001, "1"), (2, 8, 5, 262144, "1")])
 def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
-    """The experimental warp-specialised encoder (env NKFS_ENC_WS, nk8_ws.hip:
-    encoder waves + one hash wave per workgroup) writes the same parts and
-    digests as the default fused kernel, tails and partial workgroups
-    included."""
+    """The warp-specialised encoder (nk8_ws.hip: encoder waves + one hash
+    wave per workgroup; the default for n <= 8 grids of <= 1,024 fused waves,
+    forced here with NKFS_ENC_WS) writes the same parts and digests as the
+    fused kernel, tails and partial workgroups included."""
     from nkfs_amd import batch
     S = 23
     blocks = batch.synth(S, B, first=77)
     ids = dev(synth.batch_ids(S, n, first=77))
+    monkeypatch.setenv("NKFS_ENC_WS", "0")  # the fused kernel as the baseline
     p0, d0 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     monkeypatch.setenv("NKFS_ENC_WS", str(ne))
@@ -521,6 +522,7 @@ def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
     blocks = batch.synth(S, B, first=123)
     ids_np = synth.batch_ids(S, n, first=123)
     ids = dev(ids_np)
+    monkeypatch.setenv("NKFS_ENC_WS", "0")  # small grids would take the warp-specialised kernel
     monkeypatch.setenv("NKFS_NIB", "0")
     p0, d0 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
