@@ -369,6 +369,8 @@ def run_ragged(args, rank, world, device):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline_mixed(sizes, n, k, args.cpu_seconds)
+    if rank == 0 and args.pcie:
+        result["pcie_inclusive_GiBps"] = pcie_rate_ragged(batch, blocks, boff, poff, sizes, ids_np, n, k, pos, ppos)
     if rank == 0:
         print(json.dumps(result), flush=True)
     import torch.distributed as dist
@@ -404,6 +406,27 @@ def cpu_baseline_mixed(sizes, n, k, target_s):
             "sample": f"C5 mix (N={n},K={k}): per size class {list(C5_SIZES)}, nk8_split_block + XXH64 of every "
                       f"part + nk8_assemble_block from {k} survivors, {threads} pthreads, weighted by the "
                       f"batch's bytes per class, ~{target_s:.0f} s"}
+
+
+def pcie_rate_ragged(batch, blocks, boff, poff, sizes, ids_np, n, k, pos, ppos):
+    """C5 from host memory (nkfs_nk8_encode_ragged_host): pinned packed
+    blocks -> H2D -> ragged encode+XXH64 -> D2H of parts and digests, in
+    sub-batches of consecutive stripes on three streams.  User GiB/s."""
+    import torch
+    host = blocks.cpu().pin_memory()
+    bo = torch.from_numpy(boff).pin_memory()
+    po = torch.from_numpy(poff).pin_memory()
+    sz = torch.from_numpy(sizes.astype("int32")).pin_memory()
+    ids = torch.from_numpy(ids_np).pin_memory()
+    parts = torch.empty(ppos, dtype=torch.uint8).pin_memory()
+    dig = torch.empty(len(sizes) * n, dtype=torch.int64).pin_memory()
+    batch.encode_ragged_host(host, bo, sz, n, k, ids, parts, po, dig)  # warm-up
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch.encode_ragged_host(host, bo, sz, n, k, ids, parts, po, dig)
+    t1 = time.perf_counter()
+    return round(int(sizes.sum()) * reps / (t1 - t0) / 2**30, 3)
 
 
 def pmc_traffic(config):

@@ -149,6 +149,21 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch,
 			 uint64_t part_pitch, uint64_t *h_digests,
 			 uint64_t chunk_bytes);
 
+/* Host-memory form of nkfs_nk8_encode_ragged (the C5 mixed batch from page
+ * buffers): stripe s is h_block_size[s] bytes at h_blocks + h_block_off[s],
+ * part i goes to h_parts + h_part_off[s] + i*nkfs_part_pitch(
+ * h_block_size[s], k), digests to h_digests[s*n + i].  Offsets must be
+ * non-decreasing in s (-EINVAL otherwise).  Consecutive stripes of about
+ * chunk_bytes (0 = 32 MiB) flow through the GPU as one sub-batch each,
+ * H2D / kernels / D2H overlapped as nkfs_nk8_encode_host.  Synchronous. */
+int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks,
+				const uint64_t *h_block_off,
+				const uint32_t *h_block_size,
+				uint32_t max_block_size, uint32_t nstripes,
+				int n, int k, const uint8_t *h_ids,
+				uint8_t *h_parts, const uint64_t *h_part_off,
+				uint64_t *h_digests, uint64_t chunk_bytes);
+
 /* Fill a uniform batch with the seeded counter-based splitmix64 stripes of
  * nkfs_amd/synth.py (bench / test input synthesis on the device). */
 int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch,

@@ -58,6 +58,8 @@ _SIGS = {
                                          C.c_uint64, C.c_uint32, vp, vp, vp, vp, vp]),
     "nkfs_nk8_decode_ragged": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32,
                                          C.c_uint32, vp, vp, vp]),
+    "nkfs_nk8_encode_ragged_host": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, vp, vp, vp, vp,
+                                              C.c_uint64]),
     "nkfs_xxh64_batch": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint64, vp, vp]),
     "nkfs_clu_sum_batch": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, vp, vp, vp, vp]),
     "nkfs_pages_dsum_batch": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp]),

@@ -181,6 +181,27 @@ def encode_host(blocks, block_size: int, n: int, k: int, ids, chunk_bytes: int =
     return parts, dig
 
 
+def encode_ragged_host(blocks, block_off, block_sizes, n: int, k: int, ids, parts, part_off, digests=None,
+                       max_block_size: int | None = None, chunk_bytes: int = 0):
+    """Host-memory ragged encode (+XXH64): every argument a contiguous host
+    numpy array or CPU tensor (uint8 blocks/ids/parts, int64 offsets, int32
+    sizes, int64 digests or None); offsets non-decreasing in stripe order.
+    Writes parts/digests in place (nkfs_nk8_encode_ragged_host)."""
+    t = [torch.as_tensor(x) for x in (blocks, block_off, block_sizes, ids, parts, part_off)]
+    for x, dt, nm in zip(t, (U8, torch.int64, torch.int32, U8, U8, torch.int64),
+                         ("blocks", "block_off", "block_sizes", "ids", "parts", "part_off")):
+        if x.is_cuda or x.dtype != dt or not x.is_contiguous():
+            raise ValueError(f"{nm}: contiguous {dt} host array")
+    dg = None if digests is None else torch.as_tensor(digests)
+    if dg is not None and (dg.is_cuda or dg.dtype != torch.int64 or not dg.is_contiguous()):
+        raise ValueError("digests: contiguous int64 host array")
+    nstripes = t[2].numel()
+    mb = int(t[2].max()) if max_block_size is None and nstripes else (max_block_size or 1)
+    check(lib().nkfs_nk8_encode_ragged_host(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), mb, nstripes, n, k,
+                                            t[3].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), _ptr(dg),
+                                            chunk_bytes), "nkfs_nk8_encode_ragged_host")
+
+
 def xxh64_batch(base: torch.Tensor, off: torch.Tensor, lens: torch.Tensor, seed: int = 0, stream=None):
     _need(base, U8, "base")
     out = torch.empty(off.numel(), dtype=torch.int64, device=base.device)

@@ -552,3 +552,39 @@ def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
         torch.cuda.synchronize()
         outs.append((parts, dig))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,k,chunk", [(8, 5, 0), (4, 2, 1 << 20), (6, 3, 100000)])
+def test_ragged_host_pipeline(L, O, n, k, chunk):
+    """nkfs_nk8_encode_ragged_host (host memory in/out, C5 mixed sizes,
+    sub-batches of consecutive stripes overlapped on three streams) equals
+    the device-resident ragged encode, parts and digests, for pageable
+    numpy buffers and several sub-batch sizes (one stripe larger than a
+    sub-batch included)."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(37)
+    sizes[:4] = (1048576, 1, 4096, 70001)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, block_gap=8)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(500 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=500)
+    parts_d = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    dig_d = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts_d, dev(poff),
+                        dig_d, int(sizes.max()))
+    torch.cuda.synchronize()
+    parts_h = np.zeros(ppos, np.uint8)
+    dig_h = np.zeros(len(sizes) * n, np.int64)
+    batch.encode_ragged_host(host, boff, sizes.astype(np.int32), n, k, ids_np, parts_h, poff, dig_h,
+                             chunk_bytes=chunk)
+    assert np.array_equal(dig_h, dig_d.cpu().numpy())
+    pd = parts_d.cpu().numpy()
+    for s, B in enumerate(sizes):
+        pitch = batch.part_pitch(int(B), k)
+        ps = batch.part_size(int(B), k)
+        for i in range(n):
+            a = poff[s] + i * pitch
+            assert np.array_equal(parts_h[a: a + ps], pd[a: a + ps]), (s, i)
+    want = [O.xxh64(p) for p in O.encode(host[boff[3]: boff[3] + 70001], n, k, ids_np[3])]
+    assert [u64(x) for x in dig_h[3 * n: 4 * n].tolist()] == want
