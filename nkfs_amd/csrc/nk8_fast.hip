@@ -299,15 +299,24 @@ static bool store_nt()
     return e ? atoi(e) != 0 : false;
 }
 
+// NKFS_ENC_LDS_PAD=<bytes>: experiment -- extra dynamic LDS per wave, which
+// caps the waves a CU takes and so spreads a grid over more CUs
+static size_t lds_pad()
+{
+    const char *e = getenv("NKFS_ENC_LDS_PAD");
+    return e ? size_t(atoi(e)) : 0;
+}
+
 template <int E, int P, bool HASH, bool NIB>
 static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
 {
     constexpr int G = E == 4 ? 4 : 2;
     const dim3 grid((g.nstripes + G - 1) / G);
+    const size_t pad = lds_pad();
     switch (k) {
 #define NKFS_K(KK)                                                                                  \
     case KK:                                                                                        \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH, NIB>), grid, dim3(64), 0, st, g, ids, dig, nt); \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH, NIB>), grid, dim3(64), pad, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -348,8 +357,23 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // warp-specialised kernel (4 encoder waves + 1 hash wave per 2 stripes)
     // measured +3.7 / +3.8 % in two A/Bs (profiles/r01/ab_encode_decode_knobs.txt,
     // ab_ws_single_buffer.txt).  NKFS_ENC_WS=<encoder waves> forces it, 0 off.
+    //
+    // Up to 2,048 fused waves (two per SIMD) of big stripes it also beats
+    // the fused kernel in either table form: the fused kernel's 25 KB tables
+    // let only 1,536 waves reside (a second, mostly empty round beyond that)
+    // and nibble tables cost lookups where few waves share a SIMD -- N8K5
+    // 1 MiB x 3,840: fused 3.60 / nibble 4.60 / warp-specialised 4.90 TB/s,
+    // x 4,096: 3.84 / 4.76 / 5.06 (profiles/r01/ab_ws_shapes.txt).  Small
+    // parts end each stripe's hash wave soon after its table build, so the
+    // rule wants 32 KiB parts (2,048 x 64 KiB, 13 KB parts: fused 3.76,
+    // warp-specialised 3.36 TB/s; x 128 KiB: equal; ab_ws_rule.txt).  Ragged
+    // batches (sizes only on the device) keep the fused kernel.
     const u32 fused_waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
-    int ws_ne = E == 8 && fused_waves <= 1024 ? 4 : 0;
+    const u32 ps = g->block_sizes ? 0u : (g->block_size + u32(g->k) - 1) / u32(g->k);
+    u32 ws_min_part = 32768;
+    if (const char *e = getenv("NKFS_ENC_WS_MINPART"))
+        ws_min_part = u32(atoi(e));
+    int ws_ne = E == 8 && fused_waves <= 2048 && ps >= ws_min_part ? 4 : 0;
     if (const char *ws = getenv("NKFS_ENC_WS"))
         ws_ne = atoi(ws);
     if (ws_ne > 0 && digests)
@@ -361,8 +385,11 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // limit) at twice the lookups: a win where the grid offers more waves
     // than 25 KB tables let reside (C4 encode +3.2 %), a loss where one wave
     // per SIMD is issue-bound (C3 -15 %) or LDS never limited (n <= 4: -2 %)
-    // -- profiles/r01/ab_nibble_tables.txt.  NKFS_NIB=0/1 overrides.
-    bool nib = E == 8 && fused_waves >= 2048;
+    // -- profiles/r01/ab_nibble_tables.txt.  The 25 KB form lets 6 waves
+    // reside per CU (1,536 on the chip), so nibble tables take every grid
+    // beyond that (N8K5 1 MiB x 3,840: 3.60 -> 4.60 TB/s, ab_ws_shapes.txt).
+    // NKFS_NIB=0/1 overrides.
+    bool nib = E == 8 && fused_waves > 1536;
     if (const char *e = getenv("NKFS_NIB"))
         nib = atoi(e) != 0;
     const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, st, *g, ids, digests, nt)

@@ -511,6 +511,31 @@ def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
     assert torch.equal(d0, d1)
 
 
+@pytest.mark.parametrize("S,B", [(2200, 163840), (3500, 131072), (1700, 1048576)])
+def test_encode_dispatch_shapes_agree(L, O, monkeypatch, S, B):
+    """Grids the default dispatch sends to different kernels (N8K5: 1,100
+    fused waves of 32 KiB parts -> warp-specialised; 1,750 waves of 26 KB
+    parts -> nibble tables; 850 waves of 1 MiB stripes -> warp-specialised)
+    give the same parts and digests as the fused 256-entry-table kernel,
+    and the oracle's on the first and last stripe."""
+    from nkfs_amd import batch
+    n, k = 8, 5
+    blocks = batch.synth(S, B, first=5)
+    ids_np = synth.batch_ids(S, n, first=5)
+    ids = dev(ids_np)
+    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("NKFS_ENC_WS", "0")
+    monkeypatch.setenv("NKFS_NIB", "0")
+    p0, d0 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    for s in (0, S - 1):
+        want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
+        assert [u64(x) for x in d1[s * n:(s + 1) * n].cpu().tolist()] == [O.xxh64(p) for p in want]
+
+
 @pytest.mark.parametrize("n,k,B", [(8, 5, 262144), (8, 8, 4096 * 8 + 5), (6, 3, 70001), (4, 2, 4096), (3, 3, 777),
                                    (7, 2, 1)])
 def test_nibble_tables_match(L, O, monkeypatch, n, k, B):

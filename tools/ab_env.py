@@ -29,7 +29,10 @@ def main():
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(0))
     for name in cfgs:
-        S, B, n, k, _ = CONFIGS[name]
+        if name in CONFIGS:
+            S, B, n, k, _ = CONFIGS[name]
+        else:  # uniform shape "S:B:n:k", e.g. 3840:1048576:8:5
+            S, B, n, k = (int(x) for x in name.split(":"))
         ps = batch.part_size(B, k)
         blocks = batch.synth(S, B)
         ids = torch.from_numpy(synth.batch_ids(S, n)).cuda()
