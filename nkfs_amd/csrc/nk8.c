@@ -106,7 +106,7 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 	uint8_t *d = dv;
 	HIPGO(hipMemcpyAsync(d, block, B, hipMemcpyHostToDevice, c->stream));
 	HIPGO(hipMemcpyAsync(d + off_ids, ids, (size_t)n, hipMemcpyHostToDevice, c->stream));
-	struct nkfs_geom g = { d, round16(B), B, NULL, NULL, d + off_parts, pitch, NULL, 1, n, k, NULL };
+	struct nkfs_geom g = { d, round16(B), B, NULL, NULL, d + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0 };
 	if ((err = nkfs_launch_encode(&g, d + off_ids, NULL, nkfs_gf(), c->stream)))
 		goto out;
 	for (int i = 0; i < n; i++)
@@ -195,7 +195,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 	}
 	HIPGO(hipMemcpyAsync(d + off_ids, h, 512, hipMemcpyHostToDevice, c->stream));
 	struct nkfs_geom g = { d + off_block, round16(block_size), block_size, NULL, NULL, d + off_parts, pitch,
-			       NULL, 1, k, k, NULL };
+			       NULL, 1, k, k, NULL, 0, 0 };
 	if ((err = nkfs_launch_decode(&g, k, d + off_ids, d + off_avail, k, d + off_work,
 				      (int32_t *)(d + off_status), nkfs_gf(), c->stream, NULL, NULL)))
 		goto out;

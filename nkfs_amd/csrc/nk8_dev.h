@@ -185,5 +185,21 @@ __device__ inline Stripe stripe_at(const nkfs_geom &g, u32 s)
     return v;
 }
 
+// Stripe behind wave slot `slot` (g.order applied) and whether this launch
+// processes it: the slot is in range and the stripe's part size lies in the
+// launch's window [part_min, part_max) (0 = unbounded).
+__device__ inline bool slot_live(const nkfs_geom &g, u32 slot, u32 &s)
+{
+    s = slot;
+    if (slot >= g.nstripes)
+        return false;
+    if (g.order)
+        s = g.order[slot];
+    if (!g.part_min && !g.part_max)
+        return true;
+    const u32 ps = part_size_of(g.block_sizes ? g.block_sizes[s] : g.block_size, g.k);
+    return ps >= g.part_min && (!g.part_max || ps < g.part_max);
+}
+
 }  // namespace dev
 }  // namespace nkfs

@@ -67,9 +67,10 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     const int gi = lane / LP;
     const int li = lane % LP;
     const int n = g.n;
-    const u32 slot_ = blockIdx.x * G + gi;
-    const bool live = slot_ < g.nstripes;
-    const u32 s = live && g.order ? g.order[slot_] : slot_;
+    u32 s;
+    const bool live = slot_live(g, blockIdx.x * G + gi, s);
+    if (!__any(live))
+        return;  // every stripe of this wave belongs to the other launch of a split batch
     Stripe v{};
     if (live)
         v = stripe_at(g, s);
@@ -378,6 +379,32 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         ws_ne = atoi(ws);
     if (ws_ne > 0 && digests)
         return nkfs_ws_encode(g, ids, digests, ws_ne, nt, st);
+    // Ragged n <= 8 batches whose size bound allows big parts are split in
+    // two launches by part size, read on the device: stripes with parts of
+    // >= 64 KiB on the warp-specialised kernel (sorted largest first, so
+    // they fill whole workgroups), the rest on the fused kernel; each kernel
+    // skips the other's stripes (a wave or workgroup with none of its own
+    // exits at once).  The C5 mix's 1 MiB stripes alone: fused 4.32 /
+    // warp-specialised 4.53 TB/s, and the mix in one fused launch costs
+    // 300 us more than its two halves (profiles/r01/probe_c5_split.txt).
+    // NKFS_ENC_SPLIT=0 off, NKFS_ENC_SPLIT_MINPART=<bytes> moves the split.
+    nkfs_geom gs = *g;
+    if (g->block_sizes && E == 8 && digests && !g->part_min && !g->part_max) {
+        u32 split = 65536;
+        if (const char *e = getenv("NKFS_ENC_SPLIT_MINPART"))
+            split = u32(atoi(e));
+        const char *on = getenv("NKFS_ENC_SPLIT");
+        const u32 ps_bound = (g->block_size + u32(g->k) - 1) / u32(g->k);
+        if ((!on || atoi(on)) && split && ps_bound >= split) {
+            nkfs_geom gb = *g;
+            gb.part_min = split;
+            const int rc = nkfs_ws_encode(&gb, ids, digests, 4, nt, st);
+            if (rc)
+                return rc;
+            gs.part_max = split;
+            g = &gs;
+        }
+    }
     int P = 1;
     if (const char *e = getenv("NKFS_ENC_PREFETCH"))  // experiment: prefetch depth
         P = atoi(e);

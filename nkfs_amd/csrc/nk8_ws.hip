@@ -53,20 +53,24 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
 
     // chunks the workgroup iterates: the largest of its stripes' (ragged)
     u32 nch = 0;
+    bool any = false;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-        const u32 sj = blockIdx.x * S + j;
-        if (sj < g.nstripes) {
+        u32 sj;
+        if (slot_live(g, blockIdx.x * S + j, sj)) {
             const u32 psj = part_size_of(g.block_sizes ? g.block_sizes[sj] : g.block_size, K);
             nch = max(nch, (psj + CR - 1) / CR);
+            any = true;
         }
     }
+    if (!any)
+        return;  // the same for every wave of the workgroup: its stripes belong to another launch
 
     if (!hasher) {
         // ------------------------------------------------------ encoder wave
         const int gs = wave % S, sub = wave / S;
-        const u32 s = blockIdx.x * S + gs;
-        const bool live = s < g.nstripes;
+        u32 s;
+        const bool live = slot_live(g, blockIdx.x * S + gs, s);
         Stripe v{};
         if (live)
             v = stripe_at(g, s);
@@ -197,8 +201,8 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     constexpr int LPS = 64 / S;  // hash lanes per stripe (4 x E)
     const int hs = lane / LPS, hli = lane % LPS;
     const int hi = hli >> 2, ha = hli & 3;
-    const u32 s = blockIdx.x * S + hs;
-    const bool live = s < g.nstripes;
+    u32 s;
+    const bool live = slot_live(g, blockIdx.x * S + hs, s);
     u32 ps = 0;
     if (live)
         ps = part_size_of(g.block_sizes ? g.block_sizes[s] : g.block_size, K);

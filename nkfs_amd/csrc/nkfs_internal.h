@@ -30,6 +30,12 @@ struct nkfs_geom {
 	 * order[i]; NULL = identity.  Only changes which stripes share a wave and
 	 * when they run, never an output. */
 	const uint32_t *order;
+	/* optional part-size window (fast encoders only): a launch processes
+	 * only the stripes whose part size lies in [part_min, part_max), 0 =
+	 * unbounded.  Two launches with complementary windows split one ragged
+	 * batch between two kernels. */
+	uint32_t part_min;
+	uint32_t part_max;
 };
 
 /* Launchers: return 0 or a negative errno; `stream` is a hipStream_t. */

@@ -103,7 +103,7 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t
 			err = nkfs_hip_fail("H2D", (int)e);
 			goto out;
 		}
-		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k, NULL };
+		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k, NULL, 0, 0 };
 		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), s)))
 			goto out;
 		if ((e = hipMemcpyAsync(h_parts + (uint64_t)s0 * n * part_pitch, d_parts, (uint64_t)cnt * n * part_pitch,
@@ -249,7 +249,7 @@ int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks, const uint64_t *h_block
 		/* bases shifted by the range's first offsets: base + off[s] lands
 		 * inside this context's buffers */
 		struct nkfs_geom g = { d_blk - lo, 0, max_block_size, d_boff, d_sz, d_parts - plo, 0, d_poff, cnt, n, k,
-				       NULL };
+				       NULL, 0, 0 };
 		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), st)))
 			goto out;
 		if ((e = hipMemcpyAsync(h_parts + plo, d_parts, phi - plo, hipMemcpyDeviceToHost, st)) ||

@@ -230,7 +230,7 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
-			       nstripes, n, k, NULL };
+			       nstripes, n, k, NULL, 0, 0 };
 	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
 }
 
@@ -247,7 +247,7 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 	if (!d_blocks || !d_block_off || !d_block_size || !d_ids || !d_parts || !d_part_off)
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
-			       nstripes, n, k, NULL };
+			       nstripes, n, k, NULL, 0, 0 };
 	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
 }
 
@@ -271,7 +271,7 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
-			       nstripes, n_slots, k, NULL };
+			       nstripes, n_slots, k, NULL, 0, 0 };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, d_expect,
 				  d_badmask);
 }
@@ -298,7 +298,7 @@ int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off, i
 	if (!d_parts || !d_part_off || !d_ids || !d_avail || !d_blocks || !d_block_off || !d_block_size || !d_work)
 		return -EINVAL;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, (uint8_t *)d_parts, 0,
-			       d_part_off, nstripes, n_slots, k, NULL };
+			       d_part_off, nstripes, n_slots, k, NULL, 0, 0 };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, NULL, NULL);
 }
 

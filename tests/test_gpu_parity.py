@@ -613,3 +613,38 @@ def test_ragged_host_pipeline(L, O, n, k, chunk):
             assert np.array_equal(parts_h[a: a + ps], pd[a: a + ps]), (s, i)
     want = [O.xxh64(p) for p in O.encode(host[boff[3]: boff[3] + 70001], n, k, ids_np[3])]
     assert [u64(x) for x in dig_h[3 * n: 4 * n].tolist()] == want
+
+
+@pytest.mark.parametrize("n,k,gap,order", [(8, 5, 0, "1"), (8, 5, 3, "1"), (6, 3, 16, "0"), (7, 2, 0, "0")])
+def test_ragged_split_launch_matches(L, O, monkeypatch, n, k, gap, order):
+    """A ragged n <= 8 batch whose size bound allows >= 64 KiB parts is
+    encoded in two launches split by part size (warp-specialised kernel for
+    the big stripes, fused kernel for the rest).  Both halves together must
+    write exactly what one fused launch writes -- parts and digests -- for
+    sizes on either side of the split (parts of 65,535 / 65,536 bytes),
+    sorted or in batch order (NKFS_NO_ORDER), aligned or not; digests of a
+    sample against the oracle (crt/nk8.c:344-444, crt/xxhash.c:358-496)."""
+    from nkfs_amd import batch
+    sizes = np.array([k * 65536, k * 65535, 1048576, 4096, 1, 65536, k * 65536 + 1, 300000, 777] * 2, np.uint32)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, block_gap=gap)
+    hb = np.zeros(pos + 16, np.uint8)
+    for s_, Bs in enumerate(sizes):
+        hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(1300 + s_, int(Bs))
+    rid = synth.batch_ids(len(sizes), n, first=1300)
+    if order == "0":
+        monkeypatch.setenv("NKFS_NO_ORDER", "1")
+    outs = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("NKFS_ENC_SPLIT", split)
+        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+        batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff), dig,
+                            int(sizes.max()))
+        torch.cuda.synchronize()
+        outs.append((parts, dig))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    got = [u64(x) for x in outs[1][1].cpu().tolist()]
+    for s in (0, 1, 6, 7, 8):
+        B = int(sizes[s])
+        want = _oracle_digests(O, hb[None, boff[s]: boff[s] + B], rid[s:s + 1], n, k, B)
+        assert got[s * n:(s + 1) * n] == want, (s, B)

@@ -39,12 +39,15 @@ for k, cs in sorted(out.items(), key=lambda kv: -sum(kv[1].values())):
     f = cs.get("FETCH_SIZE", 0) * 1024
     w = cs.get("WRITE_SIZE", 0) * 1024
     print(f"{k[:70]:70s} FETCH {f/1e6:10.1f} MB (x2 {2*f/1e6:10.1f})  WRITE {w/1e6:10.1f} MB")
+    # one encode (decode) call may be several kernels (a ragged batch split
+    # by part size: k_encode_ws + k_encode_fast, each launched once per call),
+    # so the per-call traffic is the sum of their per-dispatch means
     for kind in ("encode", "decode"):
-        if f"k_{kind}" in k and f"{kind}_bytes_per_launch" not in rec:
-            rec[f"{kind}_kernel"] = k
-            rec[f"{kind}_bytes_per_launch"] = int(2 * f + w)
-            rec[f"{kind}_fetch_size_x2"] = int(2 * f)
-            rec[f"{kind}_write_size"] = int(w)
+        if f"k_{kind}" in k:
+            rec[f"{kind}_kernel"] = (rec[f"{kind}_kernel"] + " + " + k) if f"{kind}_kernel" in rec else k
+            for key, val in ((f"{kind}_bytes_per_launch", 2 * f + w), (f"{kind}_fetch_size_x2", 2 * f),
+                             (f"{kind}_write_size", w)):
+                rec[key] = rec.get(key, 0) + int(val)
 if a.json and a.config:
     doc = {}
     if os.path.exists(a.json):
