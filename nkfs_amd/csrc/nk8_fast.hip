@@ -339,6 +339,31 @@ static int launch_p(int P, bool nib, int k, hipStream_t st, const nkfs_geom &g, 
     return nib ? launch_k<E, 1, HASH, true>(k, st, g, ids, dig, nt) : launch_k<E, 1, HASH, false>(k, st, g, ids, dig, nt);
 }
 
+// Per-thread, per-device side stream with a fork and a join event (split
+// ragged launches, NKFS_ENC_SPLIT=2); created on first use, never freed.
+struct SideStream {
+    hipStream_t s;
+    hipEvent_t fork, join;
+};
+
+static SideStream *side_stream()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16)
+        return nullptr;
+    thread_local SideStream tab[16];
+    SideStream &ss = tab[dev];
+    if (!ss.s) {
+        if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess ||
+            hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) {
+            ss.s = nullptr;
+            return nullptr;
+        }
+    }
+    return &ss;
+}
+
 extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int ne, bool nt,
                               hipStream_t st);
 
@@ -389,13 +414,24 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // 300 us more than its two halves (profiles/r01/probe_c5_split.txt).
     // NKFS_ENC_SPLIT=0 off, NKFS_ENC_SPLIT_MINPART=<bytes> moves the split.
     nkfs_geom gs = *g;
+    hipStream_t fst = st;      // stream of the fused launch
+    SideStream *side = nullptr;  // set when the two halves of a split run concurrently
     if (g->block_sizes && E == 8 && digests && !g->part_min && !g->part_max) {
         u32 split = 65536;
         if (const char *e = getenv("NKFS_ENC_SPLIT_MINPART"))
             split = u32(atoi(e));
         const char *on = getenv("NKFS_ENC_SPLIT");
+        const int mode = on ? atoi(on) : 1;
         const u32 ps_bound = (g->block_size + u32(g->k) - 1) / u32(g->k);
-        if ((!on || atoi(on)) && split && ps_bound >= split) {
+        if (mode && split && ps_bound >= split) {
+            // mode 2: the fused half on a side stream forked from (and
+            // joined back into) the caller's stream, so its waves can fill
+            // the CUs the big half leaves idle in its last round
+            if (mode == 2 && (side = side_stream()) != nullptr) {
+                if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+                    return -EIO;
+                fst = side->s;
+            }
             nkfs_geom gb = *g;
             gb.part_min = split;
             const int rc = nkfs_ws_encode(&gb, ids, digests, 4, nt, st);
@@ -419,10 +455,12 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     bool nib = E == 8 && fused_waves > 1536;
     if (const char *e = getenv("NKFS_NIB"))
         nib = atoi(e) != 0;
-    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, st, *g, ids, digests, nt)
-                                     : launch_p<4, false>(P, nib, g->k, st, *g, ids, digests, nt))
-                          : (digests ? launch_p<8, true>(P, nib, g->k, st, *g, ids, digests, nt)
-                                     : launch_p<8, false>(P, nib, g->k, st, *g, ids, digests, nt));
+    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, fst, *g, ids, digests, nt)
+                                     : launch_p<4, false>(P, nib, g->k, fst, *g, ids, digests, nt))
+                          : (digests ? launch_p<8, true>(P, nib, g->k, fst, *g, ids, digests, nt)
+                                     : launch_p<8, false>(P, nib, g->k, fst, *g, ids, digests, nt));
+    if (side && (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess))
+        return -EIO;
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -634,7 +634,7 @@ def test_ragged_split_launch_matches(L, O, monkeypatch, n, k, gap, order):
     if order == "0":
         monkeypatch.setenv("NKFS_NO_ORDER", "1")
     outs = []
-    for split in ("0", "1"):
+    for split in ("0", "1", "2"):  # one fused launch, split, split on two streams
         monkeypatch.setenv("NKFS_ENC_SPLIT", split)
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
@@ -642,7 +642,8 @@ def test_ragged_split_launch_matches(L, O, monkeypatch, n, k, gap, order):
                             int(sizes.max()))
         torch.cuda.synchronize()
         outs.append((parts, dig))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for p_, d_ in outs[1:]:
+        assert torch.equal(outs[0][0], p_) and torch.equal(outs[0][1], d_)
     got = [u64(x) for x in outs[1][1].cpu().tolist()]
     for s in (0, 1, 6, 7, 8):
         B = int(sizes[s])

@@ -55,7 +55,7 @@ def main():
         print(f"ragged  {S} x 1 MiB        {t*1e6:9.1f} us {nb/t/1e9:7.1f} GB/s", flush=True)
         torch.cuda.empty_cache()
     sizes = synth.mixed_sizes(11520, (4096, 65536, 1048576))
-    for split in ("0", "1", "0", "1"):
+    for split in ("0", "1", "2", "0", "1", "2"):
         os.environ["NKFS_ENC_SPLIT"] = split  # read per call by the dispatch
         t, nb = ragged(sizes, n, k)
         print(f"ragged  C5 mix ({len(sizes)}) split={split} {t*1e6:9.1f} us {nb/t/1e9:7.1f} GB/s", flush=True)
