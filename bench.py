@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time the host-memory (PCIe-inclusive) path")
+    ap.add_argument("--strong-total", type=int, default=0,
+                    help="strong scaling: this many stripes in total, split evenly over the ranks "
+                         "(SURVEY.md 8(d) C3: 8192 x 1 MiB); default = the config's stripes per GPU (weak)")
     return ap.parse_args()
 
 
@@ -69,8 +72,19 @@ def dist_setup(backend: str):
 
 
 def stripe_range(rank: int, per_rank: int):
-    """Weak scaling: rank r owns stripes [r*per_rank, (r+1)*per_rank)."""
+    """Rank r owns stripes [r*per_rank, (r+1)*per_rank) (weak scaling: a
+    fixed per_rank; strong: per_rank = total / world)."""
     return rank * per_rank, per_rank
+
+
+def per_rank_stripes(config_stripes: int, strong_total: int, world: int) -> int:
+    """Stripes per rank: the config's per-GPU count (weak scaling) or an even
+    share of a fixed total (strong scaling)."""
+    if not strong_total:
+        return config_stripes
+    if strong_total % world:
+        raise SystemExit(f"--strong-total {strong_total} does not split evenly over {world} ranks")
+    return strong_total // world
 
 
 def reduce_max(value: float, device) -> float:
@@ -151,8 +165,14 @@ def main():
     _lib.check(L.nkfs_gpu_init(local), "nkfs_gpu_init")
 
     if args.config == "c5":
+        if args.strong_total:
+            raise SystemExit("--strong-total applies to the uniform configs (c2-c4)")
         return run_ragged(args, rank, world, device)
     S, B, n, k, desc = CONFIGS[args.config]
+    S = per_rank_stripes(S, args.strong_total, world)
+    if args.strong_total:
+        desc = (f"{desc.rsplit(', ', 1)[0]}, {args.strong_total} x {B // 1024} KiB stripes in total "
+                f"split over {world} GPU(s) (strong scaling)")
     first, _ = stripe_range(rank, S)
     ps = batch.part_size(B, k)
     stream = torch.cuda.current_stream(device)
@@ -225,7 +245,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong_total else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846)",
@@ -238,7 +258,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(enc_bytes / enc_s / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(args.config),
+            # PMC traffic is measured on the config's own batch; another
+            # batch size (--strong-total) has none of its own
+            "traffic": pmc_traffic(args.config) if S == CONFIGS[args.config][0] else None,
             "bytes_per_launch": enc_bytes,
             "us_per_launch": round(enc_s * 1e6, 2),
         },

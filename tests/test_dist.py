@@ -77,3 +77,16 @@ def test_single_rank_defaults(monkeypatch):
     assert bench.dist_setup("gloo") == (0, 1, 0)
     assert bench.reduce_max(3.5, torch.device("cpu")) == 3.5
     assert bench.gather_digest_xor(7, torch.device("cpu")) == [7]
+
+
+def test_strong_scaling_partition():
+    """--strong-total: a fixed total split evenly, disjoint and covering
+    (8,192 x 1 MiB over 1/2/4/8 GPUs); weak by default."""
+    assert bench.per_rank_stripes(2048, 0, 8) == 2048
+    for world in (1, 2, 4, 8):
+        per = bench.per_rank_stripes(2048, 8192, world)
+        ranges = [bench.stripe_range(r, per) for r in range(world)]
+        covered = [s for first, count in ranges for s in range(first, first + count)]
+        assert covered == list(range(8192))
+    with pytest.raises(SystemExit):
+        bench.per_rank_stripes(2048, 8192, 3)
