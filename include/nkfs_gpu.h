@@ -36,6 +36,25 @@ int nkfs_gpu_init(int device);
 /* 1 when the library has a usable GPU context. */
 int nkfs_gpu_ready(void);
 
+/* Kernel choice and launch shape of the batched entry points.  The library
+ * starts with the measured defaults; tools and tests replace
+ * them with nkfs_tune_set to compare kernels in one process.  The launchers
+ * read only this struct: no environment variable changes what runs. */
+enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC };
+enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC };
+struct nkfs_tune {
+	int enc_kernel;       /* NKFS_ENC_*: encoder for n <= 8, k <= 8 */
+	int dec_kernel;       /* NKFS_DEC_*: decoder for k <= 8 */
+	int enc_waves_per_cu; /* resident waves per CU of the walk encoder (1..32) */
+	int dec_waves_per_cu; /* resident waves per CU of the slice decoder (1..32) */
+	int dec_units;        /* 1,024-row units per slice-decoder wave (1, 2 or 4) */
+	int enc_nib;          /* walk encoder, n > 4: nibble product tables (-1 auto, 0, 1) */
+	int enc_units;        /* walk encoder: 1,024-row units per chunk (0 auto, 1, 2; n <= 4 only) */
+	int size_order;       /* ragged batches run largest stripe first (0/1) */
+};
+void nkfs_tune_get(struct nkfs_tune *t);
+int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields */
+
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */
 uint32_t nkfs_part_size(uint32_t block_size, int k);
 /* part_size rounded up to 256 bytes: the pitch ragged batches and the

@@ -26,6 +26,16 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI
 u8p = C.POINTER(C.c_uint8)
 vp = C.c_void_p
 
+
+class Tune(C.Structure):
+    """struct nkfs_tune (include/nkfs_gpu.h): kernel choice and launch shape."""
+    _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
+                                       "dec_units", "enc_nib", "enc_units", "size_order")]
+
+
+ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4}
+DEC = {"auto": 0, "slice": 1, "wave": 2, "generic": 3}
+
 # name -> (restype, argtypes)
 _SIGS = {
     "nk8_init": (C.c_int, []),
@@ -46,6 +56,8 @@ _SIGS = {
     "crt_free": (None, [vp]),
     "nkfs_gpu_init": (C.c_int, [C.c_int]),
     "nkfs_gpu_ready": (C.c_int, []),
+    "nkfs_tune_get": (None, [C.POINTER(Tune)]),
+    "nkfs_tune_set": (C.c_int, [C.POINTER(Tune)]),
     "nkfs_part_size": (C.c_uint32, [C.c_uint32, C.c_int]),
     "nkfs_part_pitch": (C.c_uint64, [C.c_uint32, C.c_int]),
     "nkfs_nk8_encode": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int, vp, vp, C.c_uint64,
@@ -113,6 +125,34 @@ def header_functions() -> list[str]:
             if m.group(1) not in names:
                 names.append(m.group(1))
     return names
+
+
+def get_tune() -> Tune:
+    t = Tune()
+    lib().nkfs_tune_get(C.byref(t))
+    return t
+
+
+class tuned:
+    """Context manager: run a block with some nkfs_tune fields replaced, e.g.
+    ``with tuned(enc_kernel=ENC["fused"]): ...`` (tests pin kernels this way;
+    the library reads no environment variable to choose one)."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+        self.saved = None
+
+    def __enter__(self):
+        self.saved = get_tune()
+        t = get_tune()
+        for k, v in self.fields.items():
+            setattr(t, k, v)
+        check(lib().nkfs_tune_set(C.byref(t)), "nkfs_tune_set")
+        return t
+
+    def __exit__(self, *exc):
+        lib().nkfs_tune_set(C.byref(self.saved))
+        return False
 
 
 def check(rc: int, what: str = "nkfs") -> int:

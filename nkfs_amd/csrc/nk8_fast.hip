@@ -293,31 +293,15 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     }
 }
 
-// NKFS_STORE_NT=0/1 overrides the default store flavour (tuning knob)
-static bool store_nt()
-{
-    const char *e = getenv("NKFS_STORE_NT");
-    return e ? atoi(e) != 0 : false;
-}
-
-// NKFS_ENC_LDS_PAD=<bytes>: experiment -- extra dynamic LDS per wave, which
-// caps the waves a CU takes and so spreads a grid over more CUs
-static size_t lds_pad()
-{
-    const char *e = getenv("NKFS_ENC_LDS_PAD");
-    return e ? size_t(atoi(e)) : 0;
-}
-
-template <int E, int P, bool HASH, bool NIB>
-static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
+template <int E, bool HASH, bool NIB>
+static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig)
 {
     constexpr int G = E == 4 ? 4 : 2;
     const dim3 grid((g.nstripes + G - 1) / G);
-    const size_t pad = lds_pad();
     switch (k) {
-#define NKFS_K(KK)                                                                                  \
-    case KK:                                                                                        \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, P, HASH, NIB>), grid, dim3(64), pad, st, g, ids, dig, nt); \
+#define NKFS_K(KK)                                                                                      \
+    case KK:                                                                                            \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, 1, HASH, NIB>), grid, dim3(64), 0, st, g, ids, dig, false); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -332,135 +316,46 @@ static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
     }
 }
 
-template <int E, bool HASH>
-static int launch_p(int P, bool nib, int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, bool nt)
-{
-    (void)P;  // depths 2-3 measured slower; only P = 1 is instantiated
-    return nib ? launch_k<E, 1, HASH, true>(k, st, g, ids, dig, nt) : launch_k<E, 1, HASH, false>(k, st, g, ids, dig, nt);
-}
-
-// Per-thread, per-device side stream with a fork and a join event (split
-// ragged launches, NKFS_ENC_SPLIT=2); created on first use, never freed.
-struct SideStream {
-    hipStream_t s;
-    hipEvent_t fork, join;
-};
-
-static SideStream *side_stream()
-{
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16)
-        return nullptr;
-    thread_local SideStream tab[16];
-    SideStream &ss = tab[dev];
-    if (!ss.s) {
-        if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess ||
-            hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) {
-            ss.s = nullptr;
-            return nullptr;
-        }
-    }
-    return &ss;
-}
-
 extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int ne, bool nt,
                               hipStream_t st);
 
-// Returns -ENOSYS when the shape is outside the fast path (the caller then
-// uses the generic kernels).
-extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *,
+// Fused encoder family for n <= 8, k <= 8.  rules != 0: the measured shape
+// rules pick the fused or the warp-specialised kernel; rules == 0: the fused
+// kernel only.  nib: -1 by rule, 0 / 1 forced (struct nkfs_tune).  Returns
+// -ENOSYS outside the fast path (the caller then uses the generic kernels).
+extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int rules, int nib,
                                 hipStream_t st)
 {
-    if (getenv("NKFS_FORCE_GENERIC"))
-        return -ENOSYS;
     if (g->n > 8 || g->k > 8)
         return -ENOSYS;
     const int E = g->n <= 4 ? 4 : 8;
-    const bool nt = store_nt();
-    // n <= 8 grids of at most one wave per SIMD (few big stripes, e.g. C3:
+    // n <= 8 grids of at most two waves per SIMD of big stripes (e.g. C3:
     // 2,048 x 1 MiB) are issue-bound in the fused kernel; there the
     // warp-specialised kernel (4 encoder waves + 1 hash wave per 2 stripes)
-    // measured +3.7 / +3.8 % in two A/Bs (profiles/r01/ab_encode_decode_knobs.txt,
-    // ab_ws_single_buffer.txt).  NKFS_ENC_WS=<encoder waves> forces it, 0 off.
-    //
-    // Up to 2,048 fused waves (two per SIMD) of big stripes it also beats
-    // the fused kernel in either table form: the fused kernel's 25 KB tables
-    // let only 1,536 waves reside (a second, mostly empty round beyond that)
-    // and nibble tables cost lookups where few waves share a SIMD -- N8K5
-    // 1 MiB x 3,840: fused 3.60 / nibble 4.60 / warp-specialised 4.90 TB/s,
-    // x 4,096: 3.84 / 4.76 / 5.06 (profiles/r01/ab_ws_shapes.txt).  Small
-    // parts end each stripe's hash wave soon after its table build, so the
-    // rule wants 32 KiB parts (2,048 x 64 KiB, 13 KB parts: fused 3.76,
-    // warp-specialised 3.36 TB/s; x 128 KiB: equal; ab_ws_rule.txt).  Ragged
-    // batches (sizes only on the device) keep the fused kernel.
+    // wins: N8K5 1 MiB x 3,840: fused 3.60 / nibble 4.60 / warp-specialised
+    // 4.90 TB/s, x 4,096: 3.84 / 4.76 / 5.06 (profiles/r01/ab_ws_shapes.txt).
+    // Small parts end each stripe's hash wave soon after its table build, so
+    // the rule wants 32 KiB parts (2,048 x 64 KiB, 13 KB parts: fused 3.76,
+    // warp-specialised 3.36 TB/s; ab_ws_rule.txt).  Ragged batches (sizes
+    // only on the device) keep the fused kernel.
     const u32 fused_waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
     const u32 ps = g->block_sizes ? 0u : (g->block_size + u32(g->k) - 1) / u32(g->k);
-    u32 ws_min_part = 32768;
-    if (const char *e = getenv("NKFS_ENC_WS_MINPART"))
-        ws_min_part = u32(atoi(e));
-    int ws_ne = E == 8 && fused_waves <= 2048 && ps >= ws_min_part ? 4 : 0;
-    if (const char *ws = getenv("NKFS_ENC_WS"))
-        ws_ne = atoi(ws);
-    if (ws_ne > 0 && digests)
-        return nkfs_ws_encode(g, ids, digests, ws_ne, nt, st);
-    // Ragged n <= 8 batches whose size bound allows big parts are split in
-    // two launches by part size, read on the device: stripes with parts of
-    // >= 64 KiB on the warp-specialised kernel (sorted largest first, so
-    // they fill whole workgroups), the rest on the fused kernel; each kernel
-    // skips the other's stripes (a wave or workgroup with none of its own
-    // exits at once).  The C5 mix's 1 MiB stripes alone: fused 4.32 /
-    // warp-specialised 4.53 TB/s, and the mix in one fused launch costs
-    // 300 us more than its two halves (profiles/r01/probe_c5_split.txt).
-    // NKFS_ENC_SPLIT=0 off, NKFS_ENC_SPLIT_MINPART=<bytes> moves the split.
-    nkfs_geom gs = *g;
-    hipStream_t fst = st;      // stream of the fused launch
-    SideStream *side = nullptr;  // set when the two halves of a split run concurrently
-    if (g->block_sizes && E == 8 && digests && !g->part_min && !g->part_max) {
-        u32 split = 65536;
-        if (const char *e = getenv("NKFS_ENC_SPLIT_MINPART"))
-            split = u32(atoi(e));
-        const char *on = getenv("NKFS_ENC_SPLIT");
-        const int mode = on ? atoi(on) : 1;
-        const u32 ps_bound = (g->block_size + u32(g->k) - 1) / u32(g->k);
-        if (mode && split && ps_bound >= split) {
-            // mode 2: the fused half on a side stream forked from (and
-            // joined back into) the caller's stream, so its waves can fill
-            // the CUs the big half leaves idle in its last round
-            if (mode == 2 && (side = side_stream()) != nullptr) {
-                if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
-                    return -EIO;
-                fst = side->s;
-            }
-            nkfs_geom gb = *g;
-            gb.part_min = split;
-            const int rc = nkfs_ws_encode(&gb, ids, digests, 4, nt, st);
-            if (rc)
-                return rc;
-            gs.part_max = split;
-            g = &gs;
-        }
-    }
-    int P = 1;
-    if (const char *e = getenv("NKFS_ENC_PREFETCH"))  // experiment: prefetch depth
-        P = atoi(e);
+    if (rules && E == 8 && digests && fused_waves <= 2048 && ps >= 32768)
+        return nkfs_ws_encode(g, ids, digests, 4, false, st);
     // Nibble tables free LDS (N8K5: 25 -> 11 KB per wave, the occupancy
     // limit) at twice the lookups: a win where the grid offers more waves
     // than 25 KB tables let reside (C4 encode +3.2 %), a loss where one wave
     // per SIMD is issue-bound (C3 -15 %) or LDS never limited (n <= 4: -2 %)
     // -- profiles/r01/ab_nibble_tables.txt.  The 25 KB form lets 6 waves
     // reside per CU (1,536 on the chip), so nibble tables take every grid
-    // beyond that (N8K5 1 MiB x 3,840: 3.60 -> 4.60 TB/s, ab_ws_shapes.txt).
-    // NKFS_NIB=0/1 overrides.
-    bool nib = E == 8 && fused_waves > 1536;
-    if (const char *e = getenv("NKFS_NIB"))
-        nib = atoi(e) != 0;
-    const int rc = E == 4 ? (digests ? launch_p<4, true>(P, nib, g->k, fst, *g, ids, digests, nt)
-                                     : launch_p<4, false>(P, nib, g->k, fst, *g, ids, digests, nt))
-                          : (digests ? launch_p<8, true>(P, nib, g->k, fst, *g, ids, digests, nt)
-                                     : launch_p<8, false>(P, nib, g->k, fst, *g, ids, digests, nt));
-    if (side && (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess))
-        return -EIO;
+    // beyond that.
+    const bool nb = nib < 0 ? E == 8 && fused_waves > 1536 : nib != 0;
+    const int rc = E == 4 ? (digests ? launch_k<4, true, false>(g->k, st, *g, ids, digests)
+                                     : launch_k<4, false, false>(g->k, st, *g, ids, digests))
+                          : nb ? (digests ? launch_k<8, true, true>(g->k, st, *g, ids, digests)
+                                          : launch_k<8, false, true>(g->k, st, *g, ids, digests))
+                               : (digests ? launch_k<8, true, false>(g->k, st, *g, ids, digests)
+                                          : launch_k<8, false, false>(g->k, st, *g, ids, digests));
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -849,7 +744,7 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
                                 int navail, int32_t *status, const void *gf, hipStream_t st,
                                 const uint64_t *expect, uint64_t *badmask)
 {
-    if (getenv("NKFS_FORCE_GENERIC") || g->k > 8 || (g->part_pitch & 15) ||
+    if (g->k > 8 || (g->part_pitch & 15) ||
         (reinterpret_cast<uintptr_t>(g->parts) & 15))
         return -ENOSYS;
     // one stripe per wave: for k 5..8 it halves the E=8 tables and lifts
@@ -857,7 +752,7 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     // k <= 4 the wave then streams one stripe's parts in 1 KiB runs (C2
     // decode 4.48 -> 5.08 TB/s over four stripes per wave, tools/ab_lib.py).
     const GfTables *t = (const GfTables *)gf;
-    const bool nt = store_nt();
+    const bool nt = false;
     const bool verify = expect != nullptr;
     const int G = 1;
     const u32 groups = (g->nstripes + G - 1) / G;
@@ -867,14 +762,11 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     // two 16-row units per lane per step (one-shot 4 KiB N4K2 stripes, half
     // the steps of long ones): decode +3 % (C2), +9 % (C3), +6 % (C4) in
     // one-process A/B (profiles/r01/ab_decode_units.txt); NKFS_DEC_U=1 = old
-    int U = verify ? 1 : 2;
-    if (const char *e = getenv("NKFS_DEC_U"))
-        U = atoi(e) == 1 || verify ? 1 : 2;
+    const int U = verify ? 1 : 2;
     const u32 R = 16u * (64u / u32(G)) * u32(U);
     const u32 steps = (ps + R - 1) / R;
-    u32 slices = 1, target = 4096;
-    if (const char *e = getenv("NKFS_DEC_WAVES"))  // experiment: wave-count target
-        target = u32(atoi(e));
+    u32 slices = 1;
+    const u32 target = 4096;
     while (!verify && groups * slices < target && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
@@ -883,11 +775,8 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
         if (verify)                                                                                               \
             hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, true>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
                                avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
-        else if (U == 2)                                                                                          \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
                                avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
     } while (0)
     switch (g->k) {

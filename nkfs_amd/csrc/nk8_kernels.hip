@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "../../include/nkfs_gpu.h"
 #include "gf256.h"
 #include "nkfs_internal.h"
 #include "xxh64_dev.h"
@@ -455,7 +456,9 @@ __global__ __launch_bounds__(256) void k_synth(u8 *blocks, u64 pitch, u32 B, u32
 
 // ----------------------------------------------------------- launchers
 
-extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, const void *gf, hipStream_t st);
+extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int rules, int nib, hipStream_t st);
+extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int ne, bool nt,
+                              hipStream_t st);
 extern "C" int nkfs_fast_xxh64_list(const u8 *base, const u64 *off, const u64 *len, u32 count, u64 seed, u64 *out,
                                     hipStream_t st);
 extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, u64 *out, hipStream_t st);
@@ -493,7 +496,7 @@ extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
 template <class F>
 static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 {
-    if (!g->block_sizes || g->order || getenv("NKFS_NO_ORDER"))
+    if (!g->block_sizes || g->order || !nkfs_g_tune.size_order)
         return -ENOSYS;
     u32 *perm = nullptr;
     if (hipMallocAsync(reinterpret_cast<void **>(&perm), size_t(g->nstripes) * sizeof(u32), st) != hipSuccess)
@@ -508,6 +511,33 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
     return rc ? rc : (e == hipSuccess ? 0 : -EIO);
 }
 
+extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,
+                                int cus, hipStream_t st);
+extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
+                                 void *work, int32_t *status, const void *gf, int units, int waves, hipStream_t st);
+
+// Fast-path encoder choice (n <= 8, k <= 8), struct nkfs_tune.enc_kernel:
+// AUTO = the fused / warp-specialised shape rules for uniform batches (the
+// walk encoder measured equal on N8K5 shapes and slower on N4K2 4 KiB,
+// DESIGN.md §4) and the walk encoder for ragged ones (one wave per stripe in
+// size order; the fused kernel would pair unequal stripes in one wave).
+static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStream_t st)
+{
+    const nkfs_tune &t = nkfs_g_tune;
+    const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel : g->block_sizes ? NKFS_ENC_WALK : NKFS_ENC_AUTO;
+    if (kern == NKFS_ENC_WALK) {
+        // two 1,024-row units per chunk for n <= 4 (a 4 KiB N4K2 stripe is one chunk)
+        const int units = g->n <= 4 ? (t.enc_units ? t.enc_units : 2) : 1;
+        const int nib = t.enc_nib < 0 ? 0 : t.enc_nib;
+        const int rc = nkfs_walk_encode(g, ids, digests, units, nib, t.enc_waves_per_cu, nkfs_cu_count(), st);
+        if (rc != -ENOSYS)
+            return rc;
+    }
+    if (kern == NKFS_ENC_WS && digests)
+        return nkfs_ws_encode(g, ids, digests, 4, false, st);
+    return nkfs_fast_encode(g, ids, digests, kern == NKFS_ENC_AUTO, t.enc_nib, st);
+}
+
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
                                   void *stream)
 {
@@ -515,10 +545,11 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         return 0;
     hipStream_t st = (hipStream_t)stream;
     int rc = -ENOSYS;
-    if (g->n <= 8 && g->k <= 8 && !getenv("NKFS_FORCE_GENERIC"))
-        rc = with_size_order(g, st, [&](const nkfs_geom *go) { return nkfs_fast_encode(go, ids, digests, gf, st); });
-    if (rc == -ENOSYS)
-        rc = nkfs_fast_encode(g, ids, digests, gf, st);
+    if (g->n <= 8 && g->k <= 8 && nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC) {
+        rc = with_size_order(g, st, [&](const nkfs_geom *go) { return fast_encode(go, ids, digests, st); });
+        if (rc == -ENOSYS)
+            rc = fast_encode(g, ids, digests, st);
+    }
     if (rc != -ENOSYS)
         return rc;
     const u32 ps = max_part_size(g, g->block_size);
@@ -533,7 +564,7 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
 
 extern "C" int nkfs_launch_hash_parts(const nkfs_geom *g, uint64_t *digests, void *stream)
 {
-    if (!getenv("NKFS_FORCE_GENERIC"))
+    if (nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC)
         return nkfs_fast_xxh64_parts(g, digests, (hipStream_t)stream);
     const u64 threads = u64(g->nstripes) * u64(g->n) * 4;
     if (!threads)
@@ -550,13 +581,25 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
+    const nkfs_tune &t = nkfs_g_tune;
     int rc = -ENOSYS;
-    if (g->k <= 8 && !getenv("NKFS_FORCE_GENERIC"))
-        rc = with_size_order(g, st, [&](const nkfs_geom *go) {
-            return nkfs_fast_decode(go, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
-        });
-    if (rc == -ENOSYS)
-        rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
+    if (g->k <= 8 && t.dec_kernel != NKFS_DEC_GENERIC) {
+        // uniform batches without the integrity check: one-shot slice waves;
+        // ragged batches and the verifying form: the wave-per-stripe decoder
+        // default: one-shot slices for k >= 3 (C3/C4 decode +10-15 %); for
+        // k = 2 a 4 KiB stripe is one wave either way and the wave decoder's
+        // in-wave inverse saves the plan launch
+        const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel : g->k >= 3 ? NKFS_DEC_SLICE : NKFS_DEC_WAVE;
+        if (kern == NKFS_DEC_SLICE && !expect && !g->block_sizes)
+            rc = nkfs_slice_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_units, t.dec_waves_per_cu,
+                                   st);
+        if (rc == -ENOSYS)
+            rc = with_size_order(g, st, [&](const nkfs_geom *go) {
+                return nkfs_fast_decode(go, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
+            });
+        if (rc == -ENOSYS)
+            rc = nkfs_fast_decode(g, n_slots, ids, avail, navail, status, gf, st, expect, badmask);
+    }
     if (rc != -ENOSYS)
         return rc;
     hipLaunchKernelGGL(k_decode_prep, dim3(g->nstripes), dim3(64), 0, st, ids, avail, n_slots, navail, g->k,
@@ -594,7 +637,7 @@ extern "C" int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 {
     if (!count)
         return 0;
-    if (!getenv("NKFS_FORCE_GENERIC"))
+    if (nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC)
         return nkfs_fast_xxh64_list(base, off, len, count, seed, out, (hipStream_t)stream);
     const u64 threads = u64(count) * 4;
     hipLaunchKernelGGL(k_xxh64_batch, dim3(u32((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, base,

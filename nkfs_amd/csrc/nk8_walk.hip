@@ -1,0 +1,790 @@
+// nk8_walk.hip -- streaming N-K kernels shaped by what MI355X's HBM rewards
+// (profiles/r02/sol_shapes.txt, tools/sol.hip):
+//
+//  * every wave owns ONE stripe, and every global load / store instruction
+//    moves one contiguous 1 KiB run of one block or part;
+//  * about 8 resident waves per CU (capped through the LDS request): the
+//    same data movement runs 6.2-6.3 TB/s at 8 waves/CU and 5.8 TB/s
+//    uncapped (C2 shape), 5.8 TB/s for whole-stripe walks at 8/CU vs
+//    5.4-5.6 at 4/CU;
+//  * no lane stores with a lane stride of more than 16 B: the decode's
+//    row-major output goes through an LDS transpose (stride-80 stores cost
+//    30 % at K = 5).
+//
+// k_encode_walk -- fused encode + XXH64 of every part (crt/nk8.c:403-420,
+//   crt/xxhash.c:358-496 with seed 0 as crt/csum.c:5).  The wave walks its
+//   stripe in chunks of R = 1024*U rows: lane l encodes rows 16l..16l+15 of
+//   each 1024-row unit (k 16-byte loads), XORs k-1 lookups of packed product
+//   tables T_m[x] = (ids_0^m x, ..., ids_{n-1}^m x) per row, transposes 16
+//   rows into 16 bytes of every part (v_perm), stores them (1 KiB per
+//   instruction) and drops them into an LDS exchange.  Lane 4i+a (i < n) is
+//   accumulator a of part i's XXH64: it folds chunk c-1 from the exchange
+//   while the wave encodes chunk c, so the hash rides along the stream.
+//   XXH64 is serial per accumulator, so a stripe has exactly 4n chains; a
+//   wave hashes one stripe with 4n active lanes (one round costs ~45 SIMD
+//   cycles whatever the active lane count, tools/sol.hip).
+//
+// k_decode_slice -- decode (crt/nk8.c:446-599) as one-shot waves: wave =
+//   one slice of 1024*U rows of one stripe; the stripe's selection and
+//   K x K inverse come precomputed from k_decode_plan (one lane per stripe).
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "../../include/nkfs_gpu.h"
+#include "gf256.h"
+#include "nk8_dev.h"
+#include "nkfs_internal.h"
+#include "xxh64_dev.h"
+
+using namespace nkfs;
+using namespace nkfs::dev;
+
+namespace {
+
+constexpr size_t LDS_PER_CU = 160 * 1024;
+
+// Launch shape that caps residency at `target` one-wave workgroups per CU:
+// the dynamic LDS request that makes only `target` fit beside the kernel's
+// static LDS, and the number of workgroups per CU that are then really
+// resident (a persistent grid must not exceed it).  Cached per kernel.
+struct Shape {
+    size_t pad;
+    int per_cu;
+};
+
+Shape occupancy_shape(const void *kern, int target)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, Shape> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({kern, target});
+    if (it != cache.end())
+        return it->second;
+    hipFuncAttributes a{};
+    size_t stat = 0;
+    if (hipFuncGetAttributes(&a, kern) == hipSuccess)
+        stat = a.sharedSizeBytes;
+    if (target < 4)
+        target = 4;  // keeps the request under the 64 KiB dynamic default
+    const size_t per = LDS_PER_CU / size_t(target);
+    Shape sh{per > stat ? per - stat : 0, target};
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64, sh.pad) == hipSuccess && occ > 0)
+        sh.per_cu = occ < target ? occ : target;
+    cache[{kern, target}] = sh;
+    return sh;
+}
+
+u32 part_size_of_host(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
+
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// bit-serial GF(2^8)/0x11B product (crt/nk8.c:54-74) in registers
+__device__ inline u32 gfm_bits(u32 a, u32 b)
+{
+    u32 r = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        r ^= a & (0u - ((b >> bit) & 1u));
+        a = ((a << 1) ^ (0x11Bu & (0u - ((a >> 7) & 1u)))) & 0xFFu;
+    }
+    return r;
+}
+
+// 16 rows starting at byte `off` of the stripe's block into d[4K] (zero
+// beyond B: the reference zero-pads the tail row, crt/nk8.c:393-398)
+template <int K>
+__device__ inline void load_rows(u32 (&d)[4 * K], const Stripe &v, u64 off, bool aligned)
+{
+    if (aligned && off + 16 * K <= v.B) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint4 t = src[q];
+            d[4 * q] = t.x;
+            d[4 * q + 1] = t.y;
+            d[4 * q + 2] = t.z;
+            d[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4 * K; ++q) {
+            u32 x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const u64 p = off + 4 * q + b;
+                if (p < v.B)
+                    x |= u32(v.blk[p]) << (8 * b);
+            }
+            d[q] = x;
+        }
+    }
+}
+
+}  // namespace
+
+constexpr u32 OOB = 0x80000000u;  // buffer offset past every num_records: load 0 / store dropped
+
+__device__ inline __amdgpu_buffer_rsrc_t rsrc(const void *base, u32 bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+
+// Persistent walk.  Wave w walks stripes w, w + grid, w + 2*grid, ...
+// (per_wave of them; ragged batches: exactly one, g.order applied), each in
+// chunks of R = 1024*U rows; every (stripe, chunk) is one task and step t
+//   1. loads task t+1 (the next chunk, or the next stripe's first),
+//   2. folds task t-1's parts into the XXH64 chains (finishing a stripe's
+//      digests after its last chunk),
+//   3. encodes task t (tables rebuilt when it starts a stripe), stores it and
+//      drops it into the exchange.
+// Every global access is a buffer load/store issued on every step
+// unconditionally (out-of-range offsets read 0 / drop the write), so the
+// compiler's s_waitcnt accounting is exact and the loads of task t+1 stay
+// in flight under steps 2-3 (the wait before task t's data covers only what
+// was issued before it).  Two register sets alternate; step 0 is peeled so
+// the loop is entered in the same state it loops back in.
+template <int K, int E, int U, bool HASH, bool NIB, bool RAGGED>
+__global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *ids, u64 *digests, u32 per_wave)
+{
+    constexpr int R = 1024 * U;                // rows per chunk
+    constexpr int SP = R + 32;                 // exchange bytes per part: 32-B skew -> conflict-free hash reads
+    constexpr int TB = (NIB ? 32 : 256) * E;   // bytes per packed table
+    constexpr int W = E / 4;                   // dwords per packed entry
+    constexpr int RPC = R / 32;                // XXH64 rounds per chain per chunk
+    __shared__ __attribute__((aligned(16))) u8 tbl[(K - 1) * TB];
+    __shared__ __attribute__((aligned(16))) u8 xbuf[HASH ? E * SP : 16];
+
+    const int li = threadIdx.x;
+    const int n = g.n;
+    const u32 grid = gridDim.x;
+
+    // ---- geometry (uniform batches: one shape; ragged: this wave's stripe)
+    u32 B, s0;
+    u64 ppitch;
+    const u8 *blk0;
+    u8 *par0;
+    if constexpr (RAGGED) {
+        s0 = g.order ? g.order[blockIdx.x] : blockIdx.x;
+        B = g.block_sizes[s0];
+        ppitch = (u64(part_size_of(B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
+        blk0 = g.blocks + g.block_off[s0];
+        par0 = g.parts + g.part_off[s0];
+    } else {
+        s0 = blockIdx.x;
+        B = g.block_size;
+        ppitch = g.part_pitch;
+        blk0 = g.blocks;
+        par0 = g.parts;
+    }
+    const u32 ps = part_size_of(B, K);
+    const u32 nch = (ps + R - 1) / R;
+    const u32 ntask = per_wave * nch;
+    auto stripe_of = [&](u32 j) { return RAGGED ? s0 : s0 + j * grid; };
+    auto blk_of = [&](u32 s) { return RAGGED ? blk0 : blk0 + u64(s) * g.block_pitch; };
+    auto par_of = [&](u32 s) { return RAGGED ? par0 : par0 + u64(s) * u64(n) * ppitch; };
+    auto task_ok = [&](u32 t, u32 j) { return t < ntask && stripe_of(j) < g.nstripes; };
+
+    // ids of this wave's stripes, staged in LDS once (per_wave <= 64)
+    __shared__ u64 idl[64];
+    {
+        u64 x = 0;
+        if (u32(li) < per_wave && stripe_of(li) < g.nstripes)
+            for (int b = 0; b < n; ++b)
+                x |= u64(ids[u64(stripe_of(li)) * n + b]) << (8 * b);
+        idl[li] = x;
+    }
+
+    const __amdgpu_buffer_rsrc_t drs = rsrc(digests, g.nstripes * u32(n) * 8u);
+    const u32 pbytes = u32(n) * u32(ppitch);
+
+    using Buf = u32[U][4 * K];
+    auto load_task = [&](Buf &x, u32 t, u32 j, u32 c) {
+        const bool ok = task_ok(t, j);
+        // num_records rounded up to a dword: the buffer unit range-checks whole
+        // dwords (a dword straddling num_records reads 0); bytes past B in it
+        // are masked below (a dword never crosses a page, so it is mapped)
+        const __amdgpu_buffer_rsrc_t r = rsrc(ok ? blk_of(stripe_of(j)) : g.blocks, (B + 3u) & ~3u);
+        const u32 cb = c * u32(R * K);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const u32 off = ok ? cb + u32((u * 1024 + 16 * li) * K + 16 * q) : OOB;
+                const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+                x[u][4 * q] = v.x;
+                x[u][4 * q + 1] = v.y;
+                x[u][4 * q + 2] = v.z;
+                x[u][4 * q + 3] = v.w;
+            }
+    };
+
+    // XXH64 lane: part hi, accumulator ha (lanes 4n.. idle)
+    const int hi = li >> 2, ha = li & 3;
+    const u8 *hsrc = xbuf + (hi < E ? hi : 0) * SP + 8 * ha;
+    const u32 nst = ps >> 5;  // whole 32-byte stripes of every part
+    const u32 left = ps & 31;
+    const u32 toff = nst * 32 - (nch - 1) * R;  // tail offset inside the last chunk
+    u64 acc = xxh_acc_init(ha, 0);
+
+    auto step = [&](Buf &cur, Buf &nxt, u32 t) {
+        // task cursors: t-1 (fold), t (encode), t+1 (load); uniform shapes
+        const u32 je = t / nch, ce = t - je * nch;
+        const u32 jl = (t + 1) / nch, cl = (t + 1) - jl * nch;
+        load_task(nxt, t + 1, jl, cl);
+
+        // fold task t-1 (predicated, straight-line: the compiler interleaves
+        // the serial rounds with this step's table lookups)
+        const u32 jf = t >= 1 ? (t - 1) / nch : 0, cf = t >= 1 ? (t - 1) - jf * nch : 0;
+        const bool fok = HASH && t >= 1 && task_ok(t - 1, jf);
+        if constexpr (HASH) {
+            const u32 rbase = fok ? cf * RPC : nst;
+#pragma unroll
+            for (int r = 0; r < RPC; ++r) {
+                const u64 w = *reinterpret_cast<const u64 *>(hsrc + 32 * r);
+                const u64 nx = xxh_round(acc, w);
+                acc = rbase + r < nst ? nx : acc;
+            }
+        }
+        if constexpr (HASH) {
+            // a stripe's last chunk was folded: its digests (merge, length,
+            // tail still in the exchange, avalanche); one digest store per
+            // step, dropped unless a stripe finished here
+            u64 dval = 0;
+            const bool fin = fok && cf == nch - 1;
+            if (fin) {
+                const int base = li & ~3;
+                const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+                const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+                u64 h = ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+                h += ps;
+                u64 tw[4] = {0, 0, 0, 0};
+                if (left) {
+                    const u64 *src = reinterpret_cast<const u64 *>(xbuf + (hi < E ? hi : 0) * SP + toff);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        tw[w] = src[w];
+                }
+                dval = xxh_tail_regs(h, tw, left);
+                acc = xxh_acc_init(ha, 0);
+            }
+            const u32 doff = fin && hi < n && ha == 0 ? (stripe_of(jf) * u32(n) + u32(hi)) * 8u : OOB;
+            const v2u dv = {u32(dval), u32(dval >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(dv, drs, doff, 0, 0);
+        }
+
+        const bool eok = task_ok(t, je);
+        u32 out[U][E][4];
+        // defined on every path, so the stores below compile to one straight
+        // run (undefined data on the !eok path invites the compiler to
+        // split them into branches, each with its own s_waitcnt)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < E; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    out[u][i][q] = 0;
+        if (eok) {
+            if (ce == 0) {
+                // packed product tables T_m, m = 1..K-1, of the stripe starting here
+                const u64 idv = idl[je];
+                u32 coef[W], idw[W];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    idw[w] = u32(idv >> (32 * w));
+                    coef[w] = idw[w];
+                }
+#pragma unroll
+                for (int m = 1; m < K; ++m) {
+                    u32 basis[8][W];
+                    make_basis<W>(basis, coef);
+                    u8 *tm = tbl + (m - 1) * TB;
+                    if constexpr (NIB) {
+                        if (li < 32) {
+                            const int val = li & 15, h = li >> 4;
+                            u32 e[W];
+#pragma unroll
+                            for (int w = 0; w < W; ++w) {
+                                u32 x = 0;
+#pragma unroll
+                                for (int b = 0; b < 4; ++b)
+                                    x ^= basis[4 * h + b][w] & (0u - u32((val >> b) & 1));
+                                e[w] = x;
+                            }
+                            if constexpr (W == 2)
+                                *reinterpret_cast<uint2 *>(tm + li * E) = make_uint2(e[0], e[1]);
+                            else
+                                *reinterpret_cast<u32 *>(tm + li * E) = e[0];
+                        }
+                    } else {
+                        build_table<W, 64>(tm, basis, li);
+                    }
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        coef[w] = gf_mul_packed(coef[w], idw[w]);
+                }
+            }
+            if (ce == nch - 1 && (B & 15)) {
+                // zero the bytes of the stripe's last 16-byte piece that lie past B
+                // (the reference zero-pads its tail row, crt/nk8.c:393-398)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int q = 0; q < 4 * K; ++q) {
+                        const u32 off = ce * u32(R * K) + u32((u * 1024 + 16 * li) * K + 4 * q);
+                        const u32 keep = off >= B ? 0u : B - off >= 4 ? 4u : B - off;
+                        cur[u][q] &= keep >= 4 ? 0xFFFFFFFFu : (1u << (8 * keep)) - 1u;
+                    }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    u32 row[4][W];
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int p0 = (4 * q + rr) * K;
+                        const u32 rep = __builtin_amdgcn_perm(0u, cur[u][p0 >> 2], 0x01010101u * u32(p0 & 3));
+#pragma unroll
+                        for (int w = 0; w < W; ++w)
+                            row[rr][w] = rep;
+#pragma unroll
+                        for (int m = 1; m < K; ++m) {
+                            const int p = p0 + m;
+                            const u32 byte = (cur[u][p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                            const u8 *tb = tbl + (m - 1) * TB;
+                            if constexpr (NIB) {
+                                const u8 *e0 = tb + (byte & 15u) * E;
+                                const u8 *e1 = tb + (16u + (byte >> 4)) * E;
+                                if constexpr (E == 8) {
+                                    const uint2 t0 = *reinterpret_cast<const uint2 *>(e0);
+                                    const uint2 t1 = *reinterpret_cast<const uint2 *>(e1);
+                                    row[rr][0] ^= t0.x ^ t1.x;
+                                    row[rr][1] ^= t0.y ^ t1.y;
+                                } else {
+                                    row[rr][0] ^= *reinterpret_cast<const u32 *>(e0) ^ *reinterpret_cast<const u32 *>(e1);
+                                }
+                            } else {
+                                const u8 *e = tb + byte * E;
+                                if constexpr (E == 8) {
+                                    const uint2 tt = *reinterpret_cast<const uint2 *>(e);
+                                    row[rr][0] ^= tt.x;
+                                    row[rr][1] ^= tt.y;
+                                } else {
+                                    row[rr][0] ^= *reinterpret_cast<const u32 *>(e);
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[u][4 * w][q], out[u][4 * w + 1][q],
+                                   out[u][4 * w + 2][q], out[u][4 * w + 3][q]);
+                }
+                if constexpr (HASH)
+#pragma unroll
+                    for (int i = 0; i < E; ++i)
+                        *reinterpret_cast<uint4 *>(xbuf + i * SP + u * 1024 + 16 * li) =
+                            make_uint4(out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]);
+            }
+        }
+        if constexpr (HASH) {
+            // this task's parts into the exchange, after the fold and the tail read
+            if (eok)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < E; ++i)
+                        *reinterpret_cast<uint4 *>(xbuf + i * SP + u * 1024 + 16 * li) =
+                            make_uint4(out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]);
+        }
+        // stores: n parts x U units of 1 KiB runs; dropped where not live
+        const __amdgpu_buffer_rsrc_t prs = rsrc(eok ? par_of(stripe_of(je)) : g.parts, pbytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32 r0 = ce * u32(R) + u32(u * 1024 + 16 * li);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const u32 off = eok && i < n && r0 < ps ? u32(i) * u32(ppitch) + r0 : OOB;
+                const v4u v = {out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, prs, off, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+
+    u32 da[U][4 * K], db[U][4 * K];
+    load_task(da, 0, 0, 0);
+    const u32 last = HASH ? ntask : ntask - 1;  // step ntask only folds
+    step(da, db, 0);
+    for (u32 t = 1;;) {
+        if (t > last)
+            break;
+        step(db, da, t++);
+        if (t > last)
+            break;
+        step(da, db, t++);
+    }
+}
+
+// ------------------------------------------------------------------ decode
+//
+// k_decode_plan: lane per stripe.  First K offered slots with distinct ids
+// (crt/nk8.c:512-537) and W = V^-1 for V[m][c] = x_c^m in closed form
+// (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) / M'(x_c) with
+// M(t) = prod_c (t + x_c)): the unique inverse, so identical to the
+// reference's Gauss-Jordan (crt/nk8.c:199-266).  plan[s] = K slots then W
+// row-major; slot byte 0xFF marks a stripe with fewer than K distinct ids.
+template <int K>
+__global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *avail, int n_slots, int navail,
+                                                     u32 nstripes, u8 *plan, int32_t *status, const GfTables *gft)
+{
+    const u32 s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nstripes)
+        return;
+    const u8 *sid = ids + u64(s) * n_slots;
+    const u8 *sav = avail + u64(s) * navail;
+    u8 *pl = plan + u64(s) * (K + K * K);
+    u32 x[K], sl[K];
+    int h = 0;
+    for (int c = 0; c < navail && h < K; ++c) {
+        const u32 slot = sav[c];
+        const u32 id = sid[slot];
+        bool dup = false;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            dup |= j < h && x[j] == id;
+        if (dup)
+            continue;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (j == h) {
+                x[j] = id;
+                sl[j] = slot;
+            }
+        ++h;
+    }
+    if (status)
+        status[s] = h < K ? -EINVAL : 0;
+    if (h < K) {
+        pl[0] = 0xFF;
+        return;
+    }
+    u32 M[K + 1];
+    M[0] = 1;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        M[c + 1] = M[c];
+#pragma unroll
+        for (int i = c; i >= 1; --i)
+            M[i] = M[i - 1] ^ gfm_bits(x[c], M[i]);
+        M[0] = gfm_bits(x[c], M[0]);
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        pl[c] = u8(sl[c]);
+        u32 q[K];
+        u32 a = M[K];
+        q[K - 1] = a;
+#pragma unroll
+        for (int i = K - 1; i >= 1; --i) {
+            a = M[i] ^ gfm_bits(x[c], a);
+            q[i - 1] = a;
+        }
+        u32 dd = 0;
+#pragma unroll
+        for (int i = K - 1; i >= 0; --i)
+            dd = gfm_bits(dd, x[c]) ^ q[i];
+        const u32 dinv = gft->inv[dd];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            pl[K + c * K + i] = u8(gfm_bits(q[i], dinv));
+    }
+}
+
+// One-shot slice: rows [slice*R, slice*R + R) of one stripe, R = 1024*U.
+// XPOSE: output rows go through LDS so every store instruction writes one
+// contiguous 1 KiB run (lane l owns 16 rows = 16K contiguous bytes; stored
+// directly that is a 16K-byte lane stride).
+template <int K, int E, int U, bool XPOSE>
+__global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, const u8 *plan, u32 slices)
+{
+    constexpr int W = E / 4;
+    constexpr int TB = 256 * E;
+    constexpr int R = 1024 * U;
+    constexpr int LS = 16 * K + (K % 2 == 0 ? 16 : 0);  // transpose bytes per lane (even K padded: bank spread)
+    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
+    __shared__ __attribute__((aligned(16))) u8 obuf[XPOSE ? 64 * LS : 16];
+
+    const int li = threadIdx.x;
+    const u32 s = blockIdx.x / slices, slice = blockIdx.x % slices;
+    if (s >= g.nstripes)
+        return;
+    const u8 *pl = plan + u64(s) * (K + K * K);
+    const u32 sl0 = pl[0];
+    if (sl0 == 0xFF)
+        return;  // fewer than K distinct ids: status says -EINVAL, block untouched
+    const u32 B = g.block_size;
+    const u32 ps = part_size_of(B, K);
+    const u32 rbase = slice * R;
+    const u8 *pbase = g.parts + u64(s) * n_slots * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+
+    // loads first (their latency hides under the table build)
+    const u8 *src[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+        src[c] = pbase + u64(c ? pl[c] : sl0) * g.part_pitch;
+    u32 pv[U][K][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32 r0 = rbase + u * 1024 + 16 * li;
+        if (r0 < ps)
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
+                pv[u][c][0] = t.x;
+                pv[u][c][1] = t.y;
+                pv[u][c][2] = t.z;
+                pv[u][c][3] = t.w;
+            }
+    }
+    // U_c[x] = (W[c][0] x, ..., W[c][K-1] x), packed
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        u32 rw[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            u32 x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (4 * w + b < K)
+                    x |= u32(pl[K + c * K + 4 * w + b]) << (8 * b);
+            rw[w] = x;
+        }
+        u32 basis[8][W];
+        make_basis<W>(basis, rw);
+        build_table<W, 64>(tbl + c * TB, basis, li);
+    }
+    __syncthreads();
+
+    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32 ru = rbase + u * 1024;  // first row of this unit
+        if (ru >= ps)
+            break;
+        const u32 r0 = ru + 16 * li;
+        u32 o[4 * K];
+        if (r0 < ps) {
+            u32 tdep = 0;
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                u32 row[4 * W];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int r = 4 * gq + rr;
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        row[rr * W + w] = 0;
+#pragma unroll
+                    for (int c = 0; c < K; ++c) {
+                        const u32 byte = (pv[u][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                        const u8 *e = tbl + tdep + c * TB + byte * E;
+                        if constexpr (E == 8) {
+                            const uint2 t = *reinterpret_cast<const uint2 *>(e);
+                            row[rr * W] ^= t.x;
+                            row[rr * W + 1] ^= t.y;
+                        } else {
+                            row[rr * W] ^= *reinterpret_cast<const u32 *>(e);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    o[gq * K + q] = pack_dword<K, W>(row, q);
+                if constexpr (K * W > 8)
+                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(o[gq * K]));
+            }
+        }
+        const u64 ubyte = u64(ru) * K;  // first output byte of the unit
+        if constexpr (XPOSE) {
+            if (r0 < ps)
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    *reinterpret_cast<uint4 *>(obuf + li * LS + 16 * q) =
+                        make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const int j = q * 64 + li;  // 16-byte piece of the unit's output
+                const uint4 t = *reinterpret_cast<const uint4 *>(obuf + (j / K) * LS + (j % K) * 16);
+                const u64 off = ubyte + u64(j) * 16;
+                if (aligned && off + 16 <= B) {
+                    store16(out + off, t.x, t.y, t.z, t.w, false);
+                } else if (off < B) {
+                    const u32 tw[4] = {t.x, t.y, t.z, t.w};
+                    for (int b = 0; b < 16 && off + b < B; ++b)
+                        out[off + b] = u8(tw[b >> 2] >> (8 * (b & 3)));
+                }
+            }
+            __syncthreads();
+        } else if (r0 < ps) {
+            const u64 off = u64(r0) * K;
+            if (aligned && off + 16 * K <= B) {
+                uint4 *dst = reinterpret_cast<uint4 *>(out + off);
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    store16(dst + q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], false);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4 * K; ++q)
+                    for (int b = 0; b < 4; ++b)
+                        if (off + 4 * q + b < B)
+                            out[off + 4 * q + b] = u8(o[q] >> (8 * b));
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------- launchers
+
+template <int K, int E, int U, bool HASH, bool NIB>
+static void launch_walk_kk(hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
+{
+    // uniform batches: persistent grid of the resident waves, walking stripes
+    // grid-stride (at most 64 stripes per wave: their ids are staged in LDS);
+    // ragged: one wave per stripe
+    if (g.block_sizes) {
+        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, HASH, NIB, true>),
+                                         waves);
+        hipLaunchKernelGGL((k_encode_walk<K, E, U, HASH, NIB, true>), dim3(g.nstripes), dim3(64), sh.pad, st, g, ids,
+                           dig, 1u);
+        return;
+    }
+    const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, HASH, NIB, false>), waves);
+    const u32 cap = u32(cus) * u32(sh.per_cu);
+    u32 grid = g.nstripes < cap ? g.nstripes : cap;
+    u32 per_wave = (g.nstripes + grid - 1) / grid;
+    if (per_wave > 64) {
+        per_wave = 64;
+        grid = (g.nstripes + 63) / 64;
+    }
+    hipLaunchKernelGGL((k_encode_walk<K, E, U, HASH, NIB, false>), dim3(grid), dim3(64), sh.pad, st, g, ids, dig,
+                       per_wave);
+}
+
+template <int E, int U, bool HASH, bool NIB>
+static int launch_walk_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
+{
+    switch (k) {
+    case 2: launch_walk_kk<2, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 3: launch_walk_kk<3, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 4: launch_walk_kk<4, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 5: launch_walk_kk<5, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 6: launch_walk_kk<6, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 7: launch_walk_kk<7, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 8: launch_walk_kk<8, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    default: return -ENOSYS;
+    }
+}
+
+// Walk encoder for n <= 8, k <= 8 (uniform or ragged; g->order honoured).
+// units: 1,024-row units per chunk.  -ENOSYS where the buffer offsets of a
+// stripe would not fit 31 bits (the generic kernels take those).
+extern "C" int nkfs_walk_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int units, int nib,
+                                int waves, int cus, hipStream_t st)
+{
+    if (g->n > 8 || g->k > 8 || g->part_min || g->part_max)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    const u64 ps = part_size_of_host(g->block_size, g->k);
+    const u64 pitch = g->block_sizes ? ((ps + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1)) : g->part_pitch;
+    if (u64(g->block_size) + 2048u * 8u > 0x7FFFFFFFull || u64(g->n) * pitch > 0x7FFFFFFFull ||
+        u64(g->nstripes) * u64(g->n) * 8u > 0xFFFFFFFFull)
+        return -ENOSYS;
+    const bool h = digests != nullptr;
+    int rc;
+    if (g->n <= 4)
+        rc = units == 2 ? (h ? launch_walk_k<4, 2, true, false>(g->k, st, *g, ids, digests, waves, cus)
+                             : launch_walk_k<4, 2, false, false>(g->k, st, *g, ids, digests, waves, cus))
+                        : (h ? launch_walk_k<4, 1, true, false>(g->k, st, *g, ids, digests, waves, cus)
+                             : launch_walk_k<4, 1, false, false>(g->k, st, *g, ids, digests, waves, cus));
+    else if (nib)
+        rc = h ? launch_walk_k<8, 1, true, true>(g->k, st, *g, ids, digests, waves, cus)
+               : launch_walk_k<8, 1, false, true>(g->k, st, *g, ids, digests, waves, cus);
+    else
+        rc = h ? launch_walk_k<8, 1, true, false>(g->k, st, *g, ids, digests, waves, cus)
+               : launch_walk_k<8, 1, false, false>(g->k, st, *g, ids, digests, waves, cus);
+    if (rc)
+        return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+template <int K, int E, int U, bool XP>
+static void launch_slice(hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *plan, u32 slices, int waves)
+{
+    const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_slice<K, E, U, XP>), waves);
+    hipLaunchKernelGGL((k_decode_slice<K, E, U, XP>), dim3(g.nstripes * slices), dim3(64), sh.pad, st, g, n_slots,
+                       plan, slices);
+}
+
+template <int K, int E>
+static void launch_slice_u(int units, hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *plan, u32 slices,
+                           int waves)
+{
+    constexpr bool XP = K >= 3;
+    if (units >= 4)
+        launch_slice<K, E, 4, XP>(st, g, n_slots, plan, slices, waves);
+    else if (units == 2)
+        launch_slice<K, E, 2, XP>(st, g, n_slots, plan, slices, waves);
+    else
+        launch_slice<K, E, 1, XP>(st, g, n_slots, plan, slices, waves);
+}
+
+// Slice decoder for a uniform batch, k <= 8: plan kernel (selection +
+// inverse per stripe into `work`, nkfs_decode_work_bytes layout) then
+// one-shot slice waves.  -ENOSYS outside its shapes.
+extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
+                                 int navail, void *work, int32_t *status, const void *gf, int units, int waves,
+                                 hipStream_t st)
+{
+    if (g->k > 8 || g->block_sizes || (g->part_pitch & 15) || (reinterpret_cast<uintptr_t>(g->parts) & 15))
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    u8 *plan = static_cast<u8 *>(work);
+    const GfTables *gft = static_cast<const GfTables *>(gf);
+    const dim3 pgrid((g->nstripes + 255) / 256);
+    const u32 ps = part_size_of_host(g->block_size, g->k);
+    units = units >= 4 ? 4 : units >= 2 ? 2 : 1;
+    // a stripe that fits in fewer units takes one wave of just those
+    while (units > 1 && u32(units / 2) * 1024u >= ps)
+        units /= 2;
+    const u32 slices = (ps + 1024u * units - 1) / (1024u * units);
+    switch (g->k) {
+#define NKFS_DK(KK, EE)                                                                                          \
+    case KK:                                                                                                     \
+        hipLaunchKernelGGL((k_decode_plan<KK>), pgrid, dim3(256), 0, st, ids, avail, n_slots, navail, g->nstripes, \
+                           plan, status, gft);                                                                   \
+        launch_slice_u<KK, EE>(units, st, *g, n_slots, plan, slices, waves);                                     \
+        break;
+        NKFS_DK(2, 4)
+        NKFS_DK(3, 4)
+        NKFS_DK(4, 4)
+        NKFS_DK(5, 8)
+        NKFS_DK(6, 8)
+        NKFS_DK(7, 8)
+        NKFS_DK(8, 8)
+#undef NKFS_DK
+    default:
+        return -ENOSYS;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

@@ -312,17 +312,13 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
 {
     if (g->n > 8 || g->k > 8 || !digests)
         return -ENOSYS;
-    const char *e = getenv("NKFS_ENC_WS_SB");  // single-buffered exchange (n <= 4: ne = 4; n <= 8: ne = 2)
-    const bool sb = e && atoi(e);
     int rc;
     if (g->n <= 4)
-        rc = sb ? launch_ws<4, 4, true>(g->k, st, *g, ids, digests, nt)
-                : (ne == 8 ? launch_ws<4, 8, false>(g->k, st, *g, ids, digests, nt)
-                           : launch_ws<4, 4, false>(g->k, st, *g, ids, digests, nt));
+        rc = ne == 8 ? launch_ws<4, 8, false>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<4, 4, false>(g->k, st, *g, ids, digests, nt);
     else
-        rc = sb ? launch_ws<8, 2, true>(g->k, st, *g, ids, digests, nt)
-                : (ne == 4 ? launch_ws<8, 4, false>(g->k, st, *g, ids, digests, nt)
-                           : launch_ws<8, 2, false>(g->k, st, *g, ids, digests, nt));
+        rc = ne == 4 ? launch_ws<8, 4, false>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<8, 2, false>(g->k, st, *g, ids, digests, nt);
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -38,6 +38,11 @@ struct nkfs_geom {
 	uint32_t part_max;
 };
 
+/* Kernel choice and launch shape (struct nkfs_tune, include/nkfs_gpu.h):
+ * one process-wide copy, set at init, read by the launchers. */
+struct nkfs_tune;
+extern struct nkfs_tune nkfs_g_tune;
+
 /* Launchers: return 0 or a negative errno; `stream` is a hipStream_t. */
 int nkfs_launch_gf_init(void *gf_tables, void *stream);
 int nkfs_launch_encode(const struct nkfs_geom *g, const uint8_t *ids,
@@ -72,6 +77,9 @@ int nkfs_launch_synth(uint8_t *blocks, uint64_t block_pitch,
  * the drop-in entry points): part_size rounded up to whole 256-byte spans so
  * that every chunk a kernel writes covers full 128-byte cache lines. */
 #define NKFS_PART_ALIGN 256u
+
+/* Compute units of the library's device (persistent grids). */
+int nkfs_cu_count(void);
 
 /* Sizes shared by host and launchers. */
 uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k);

@@ -24,8 +24,40 @@
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_ready;
 static int g_device = -1;
+static int g_cus = 256;
 static void *g_gf;
 static struct nkfs_ctx *g_pool;
+
+/* Measured defaults; nkfs_tune_set replaces them. */
+struct nkfs_tune nkfs_g_tune = {
+	.enc_kernel = NKFS_ENC_AUTO,
+	.dec_kernel = NKFS_DEC_AUTO,
+	.enc_waves_per_cu = 8,
+	.dec_waves_per_cu = 12,
+	.dec_units = 2,
+	.enc_nib = -1,
+	.enc_units = 0,
+	.size_order = 1,
+};
+
+void nkfs_tune_get(struct nkfs_tune *t)
+{
+	if (t)
+		*t = nkfs_g_tune;
+}
+
+int nkfs_tune_set(const struct nkfs_tune *t)
+{
+	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_GENERIC || t->dec_kernel < NKFS_DEC_AUTO ||
+	    t->dec_kernel > NKFS_DEC_GENERIC || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
+	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
+	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
+	    t->enc_units < 0 || t->enc_units > 2 ||
+	    (t->size_order != 0 && t->size_order != 1))
+		return -EINVAL;
+	nkfs_g_tune = *t;
+	return 0;
+}
 
 int nkfs_hip_fail(const char *what, int err)
 {
@@ -78,6 +110,9 @@ int nkfs_gpu_init(int device)
 		g_gf = NULL;
 		goto out;
 	}
+	int cus = 0;
+	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+		g_cus = cus;
 	g_device = device;
 	g_ready = 1;
 out:
@@ -86,6 +121,8 @@ out:
 }
 
 int nkfs_gpu_ready(void) { return g_ready; }
+
+int nkfs_cu_count(void) { return g_cus; }
 
 const void *nkfs_gf(void) { return g_gf; }
 

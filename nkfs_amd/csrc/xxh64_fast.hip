@@ -412,9 +412,6 @@ __global__ __launch_bounds__(64) void k_xxh64_ring(Src src, u64 seed, u64 *out, 
 // Register form below ~this many waves per SIMD, ring form under it.
 static bool use_ring(u64 messages)
 {
-    const char *e = getenv("NKFS_XXH_RING");  // A/B knob: 0 / 1 forces a form
-    if (e)
-        return atoi(e) != 0;
     return (messages + MSGS - 1) / MSGS <= 2048;  // <= 2 waves per SIMD
 }
 

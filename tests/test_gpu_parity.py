@@ -488,23 +488,39 @@ def test_decode_verify(L, S, B, n, k):
     assert torch.equal(out[s_unused], blocks[s_unused, :B])
 
 
-@pytest.mark.parametrize("ne,n,k,B,sb", [(4, 4, 2, 4096, "0"), (8, 4, 3, 70001, "0"), (2, 8, 5, 262144, "0"),
-                                         (4, 8, 6, 1000, "0"), (4, 4, 2, 70001, "1"), (2, 8, 5, 262144, "1")])
-def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
+ENC = None  # set lazily: nkfs_amd._lib.ENC / DEC kernel ids
+
+
+def _tuned(**kw):
+    from nkfs_amd import _lib
+    return _lib.tuned(**kw)
+
+
+def _enc(name):
+    from nkfs_amd import _lib
+    return _lib.ENC[name]
+
+
+def _dec(name):
+    from nkfs_amd import _lib
+    return _lib.DEC[name]
+
+
+@pytest.mark.parametrize("n,k,B", [(4, 2, 4096), (4, 3, 70001), (8, 5, 262144), (8, 6, 1000)])
+def test_warp_specialised_encode_matches(L, n, k, B):
     """The warp-specialised encoder (nk8_ws.hip: encoder waves + one hash
-    wave per workgroup; the default for n <= 8 grids of <= 1,024 fused waves,
-    forced here with NKFS_ENC_WS) writes the same parts and digests as the
-    fused kernel, tails and partial workgroups included."""
+    wave per workgroup; chosen by the shape rules for grids of <= 2 waves
+    per SIMD of big stripes, forced here through struct nkfs_tune) writes the
+    same parts and digests as the fused kernel, tails and partial
+    workgroups included."""
     from nkfs_amd import batch
     S = 23
     blocks = batch.synth(S, B, first=77)
     ids = dev(synth.batch_ids(S, n, first=77))
-    monkeypatch.setenv("NKFS_ENC_WS", "0")  # the fused kernel as the baseline
-    p0, d0 = batch.encode(blocks, B, n, k, ids)
-    torch.cuda.synchronize()
-    monkeypatch.setenv("NKFS_ENC_WS", str(ne))
-    monkeypatch.setenv("NKFS_ENC_WS_SB", sb)
-    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("fused")):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("ws")):
+        p1, d1 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps])
@@ -512,47 +528,121 @@ def test_warp_specialised_encode_matches(L, monkeypatch, ne, n, k, B, sb):
 
 
 @pytest.mark.parametrize("S,B", [(2200, 163840), (3500, 131072), (1700, 1048576)])
-def test_encode_dispatch_shapes_agree(L, O, monkeypatch, S, B):
+def test_encode_dispatch_shapes_agree(L, O, S, B):
     """Grids the default dispatch sends to different kernels (N8K5: 1,100
     fused waves of 32 KiB parts -> warp-specialised; 1,750 waves of 26 KB
-    parts -> nibble tables; 850 waves of 1 MiB stripes -> warp-specialised)
-    give the same parts and digests as the fused 256-entry-table kernel,
-    and the oracle's on the first and last stripe."""
+    parts -> nibble tables; 850 waves of 1 MiB stripes -> warp-specialised),
+    and the walk encoder, give the same parts and digests as the fused
+    256-entry-table kernel, and the oracle's on the first and last stripe."""
     from nkfs_amd import batch
     n, k = 8, 5
     blocks = batch.synth(S, B, first=5)
     ids_np = synth.batch_ids(S, n, first=5)
     ids = dev(ids_np)
     p1, d1 = batch.encode(blocks, B, n, k, ids)
-    torch.cuda.synchronize()
-    monkeypatch.setenv("NKFS_ENC_WS", "0")
-    monkeypatch.setenv("NKFS_NIB", "0")
-    p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("fused"), enc_nib=0):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("walk")):
+        p2, d2 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    assert torch.equal(p0[:, :ps], p2[:, :ps]) and torch.equal(d0, d2)
     for s in (0, S - 1):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
         assert [u64(x) for x in d1[s * n:(s + 1) * n].cpu().tolist()] == [O.xxh64(p) for p in want]
 
 
+@pytest.mark.parametrize("n,k,B,S,waves", [(4, 2, 4096, 3000, 4), (8, 5, 8192, 2500, 4), (8, 5, 4096, 1500, 4),
+                                           (8, 5, 9999, 1100, 4), (7, 3, 70001, 40, 8), (6, 4, 1000, 2100, 4),
+                                           (8, 8, 777, 900, 4), (2, 2, 1, 5, 8), (8, 5, 13, 3, 8),
+                                           (4, 2, 8192 + 4, 1500, 4), (5, 5, 1048576 + 3, 3, 8)])
+def test_walk_encode_matches(L, O, n, k, B, S, waves):
+    """The persistent walk encoder (nk8_walk.hip: one wave walks its stripes
+    chunk by chunk, grid-stride, fused XXH64) equals the fused kernel and the
+    oracle, parts and digests, with and without digests: several stripes per
+    wave (waves per CU capped low so the grid is smaller than the batch),
+    several chunks per stripe, tails of every size (B not a multiple of 4,
+    16 or k), one-byte blocks."""
+    from nkfs_amd import batch
+    blocks = batch.synth(S, B, first=321)
+    ids_np = synth.batch_ids(S, n, first=321)
+    ids = dev(ids_np)
+    with _tuned(enc_kernel=_enc("fused")):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("walk"), enc_waves_per_cu=waves):
+        p1, d1 = batch.encode(blocks, B, n, k, ids)
+        p2, _ = batch.encode(blocks, B, n, k, ids, digests=False)
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    assert torch.equal(p0[:, :ps], p2[:, :ps])
+    host = blocks.cpu().numpy()
+    got = [u64(x) for x in d1.cpu().tolist()]
+    for s in sorted({0, S // 2, S - 1}):
+        want = O.encode(host[s, :B], n, k, ids_np[s])
+        assert np.array_equal(p1[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want))
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want]
+
+
+@pytest.mark.parametrize("n,k,B,S", [(4, 2, 4096, 300), (8, 5, 262144, 40), (8, 5, 1048576, 9), (6, 3, 70001, 33),
+                                     (8, 8, 777, 100), (5, 4, 4099, 64), (3, 3, 1, 7), (8, 7, 65536 * 7 + 5, 5)])
+def test_slice_decode_matches(L, O, n, k, B, S):
+    """The one-shot slice decoder (nk8_walk.hip: k_decode_plan selects the
+    first k distinct offered ids and inverts per stripe, k_decode_slice
+    rebuilds 1,024-row units per wave through an LDS transpose) rebuilds the
+    same blocks as the wave decoder, for 1, 2 and 4 units per wave, tails of
+    every size, duplicate and too-few ids (status -EINVAL, block left
+    untouched, crt/nk8.c:512-537)."""
+    from nkfs_amd import batch
+    blocks = batch.synth(S, B, first=11)
+    ids_np = synth.batch_ids(S, n, first=11)
+    ids = dev(ids_np)
+    parts, _ = batch.encode(blocks, B, n, k, ids)
+    av = synth.batch_survivors(S, n, k, first=11)
+    # every slot offered: the survivors first, then the rest; stripe 1's
+    # second offered slot repeats the first one's id (the selection skips it
+    # and takes the next), stripe 2 offers a single distinct id (-EINVAL)
+    av = np.stack([np.concatenate([r, [j for j in range(n) if j not in r]]) for r in av]).astype(np.uint8)
+    ids_np2 = ids_np.copy()
+    if S > 2:
+        ids_np2[1, av[1, 1]] = ids_np2[1, av[1, 0]]
+        ids_np2[2, :] = ids_np2[2, 0]
+    outs = []
+    for kern, units in (("wave", 2), ("slice", 1), ("slice", 2), ("slice", 4)):
+        with _tuned(dec_kernel=_dec(kern), dec_units=units):
+            out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
+            o, st = batch.decode(parts, n, dev(ids_np2), dev(np.ascontiguousarray(av)), k, B, out=out)
+            torch.cuda.synchronize()
+            outs.append((out.clone(), st.cpu().tolist()))
+    for o, st in outs[1:]:
+        assert st == outs[0][1]
+        assert torch.equal(o, outs[0][0])
+    st = outs[0][1]
+    for s in range(S):
+        if s == 2 or (s == 1 and n == k):
+            continue  # stripe 1 with n == k has no spare slot to take instead
+        assert st[s] == 0 and torch.equal(outs[0][0][s], blocks[s, :B]), s
+    if S > 2:
+        assert st[2] == -22 and bool((outs[0][0][2] == 0xEE).all())
+
+
 @pytest.mark.parametrize("n,k,B", [(8, 5, 262144), (8, 8, 4096 * 8 + 5), (6, 3, 70001), (4, 2, 4096), (3, 3, 777),
                                    (7, 2, 1)])
-def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
-    """Encode with nibble product tables (NKFS_NIB=1; on by default for
-    large n <= 8 grids) equals the 256-entry-table kernel and the oracle,
-    parts and digests, uniform and ragged (size-ordered) batches."""
+def test_nibble_tables_match(L, O, n, k, B):
+    """Encode with nibble product tables (struct nkfs_tune enc_nib = 1; on by
+    rule for large n <= 8 grids of the fused kernel) equals the 256-entry-
+    table kernel and the oracle, parts and digests, uniform and ragged
+    (size-ordered) batches, fused and walk encoders."""
     from nkfs_amd import batch
     S = 20
     blocks = batch.synth(S, B, first=123)
     ids_np = synth.batch_ids(S, n, first=123)
     ids = dev(ids_np)
-    monkeypatch.setenv("NKFS_ENC_WS", "0")  # small grids would take the warp-specialised kernel
-    monkeypatch.setenv("NKFS_NIB", "0")
-    p0, d0 = batch.encode(blocks, B, n, k, ids)
-    torch.cuda.synchronize()
-    monkeypatch.setenv("NKFS_NIB", "1")
-    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("fused"), enc_nib=0):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("fused"), enc_nib=1):
+        p1, d1 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
@@ -560,7 +650,7 @@ def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
     for s in (0, S - 1):
         want = O.encode(host[s, :B], n, k, ids_np[s])
         assert [u64(x) for x in d1[s * n:(s + 1) * n].cpu().tolist()] == [O.xxh64(p) for p in want]
-    # ragged: mixed sizes through the same tables
+    # ragged: mixed sizes through the same tables, both encoders
     sizes = np.array([B, 1, 4096, 65536, B // 3 + 1] * 3, np.uint32)
     boff, poff, pos, ppos = _ragged_layout(sizes, n, k)
     hb = np.zeros(pos + 16, np.uint8)
@@ -568,15 +658,17 @@ def test_nibble_tables_match(L, O, monkeypatch, n, k, B):
         hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(900 + s_, int(Bs))
     rid = synth.batch_ids(len(sizes), n, first=900)
     outs = []
-    for nib in ("0", "1"):
-        monkeypatch.setenv("NKFS_NIB", nib)
-        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
-        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-        batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff), dig,
-                            int(sizes.max()))
-        torch.cuda.synchronize()
-        outs.append((parts, dig))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for kern in ("fused", "walk"):
+        for nib in (0, 1):
+            with _tuned(enc_kernel=_enc(kern), enc_nib=nib):
+                parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+                dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+                batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff),
+                                    dig, int(sizes.max()))
+                torch.cuda.synchronize()
+                outs.append((parts, dig))
+    for p_, d_ in outs[1:]:
+        assert torch.equal(outs[0][0], p_) and torch.equal(outs[0][1], d_)
 
 
 @pytest.mark.parametrize("n,k,chunk", [(8, 5, 0), (4, 2, 1 << 20), (6, 3, 100000)])
@@ -615,15 +707,14 @@ def test_ragged_host_pipeline(L, O, n, k, chunk):
     assert [u64(x) for x in dig_h[3 * n: 4 * n].tolist()] == want
 
 
-@pytest.mark.parametrize("n,k,gap,order", [(8, 5, 0, "1"), (8, 5, 3, "1"), (6, 3, 16, "0"), (7, 2, 0, "0")])
-def test_ragged_split_launch_matches(L, O, monkeypatch, n, k, gap, order):
-    """A ragged n <= 8 batch whose size bound allows >= 64 KiB parts is
-    encoded in two launches split by part size (warp-specialised kernel for
-    the big stripes, fused kernel for the rest).  Both halves together must
-    write exactly what one fused launch writes -- parts and digests -- for
-    sizes on either side of the split (parts of 65,535 / 65,536 bytes),
-    sorted or in batch order (NKFS_NO_ORDER), aligned or not; digests of a
-    sample against the oracle (crt/nk8.c:344-444, crt/xxhash.c:358-496)."""
+@pytest.mark.parametrize("n,k,gap,order", [(8, 5, 0, 1), (8, 5, 3, 1), (6, 3, 16, 0), (7, 2, 0, 0)])
+def test_ragged_kernels_match(L, O, n, k, gap, order):
+    """A ragged n <= 8 batch (sizes on either side of 64 KiB parts, 1 MiB,
+    4 KiB, 1 byte, odd sizes) gives the same parts and digests from the walk
+    encoder (the ragged default: one wave per stripe), the fused kernel and
+    the warp-specialised kernel, launched largest-first or in batch order
+    (struct nkfs_tune size_order), aligned or not; digests of a sample
+    against the oracle (crt/nk8.c:344-444, crt/xxhash.c:358-496)."""
     from nkfs_amd import batch
     sizes = np.array([k * 65536, k * 65535, 1048576, 4096, 1, 65536, k * 65536 + 1, 300000, 777] * 2, np.uint32)
     boff, poff, pos, ppos = _ragged_layout(sizes, n, k, block_gap=gap)
@@ -631,20 +722,18 @@ def test_ragged_split_launch_matches(L, O, monkeypatch, n, k, gap, order):
     for s_, Bs in enumerate(sizes):
         hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(1300 + s_, int(Bs))
     rid = synth.batch_ids(len(sizes), n, first=1300)
-    if order == "0":
-        monkeypatch.setenv("NKFS_NO_ORDER", "1")
     outs = []
-    for split in ("0", "1", "2"):  # one fused launch, split, split on two streams
-        monkeypatch.setenv("NKFS_ENC_SPLIT", split)
-        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
-        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-        batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff), dig,
-                            int(sizes.max()))
-        torch.cuda.synchronize()
-        outs.append((parts, dig))
+    for kern in ("walk", "fused", "ws"):
+        with _tuned(enc_kernel=_enc(kern), size_order=order):
+            parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+            dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+            batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff),
+                                dig, int(sizes.max()))
+            torch.cuda.synchronize()
+            outs.append((parts, dig))
     for p_, d_ in outs[1:]:
         assert torch.equal(outs[0][0], p_) and torch.equal(outs[0][1], d_)
-    got = [u64(x) for x in outs[1][1].cpu().tolist()]
+    got = [u64(x) for x in outs[0][1].cpu().tolist()]
     for s in (0, 1, 6, 7, 8):
         B = int(sizes[s])
         want = _oracle_digests(O, hb[None, boff[s]: boff[s] + B], rid[s:s + 1], n, k, B)
