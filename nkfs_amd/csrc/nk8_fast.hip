@@ -340,7 +340,10 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // only on the device) keep the fused kernel.
     const u32 fused_waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
     const u32 ps = g->block_sizes ? 0u : (g->block_size + u32(g->k) - 1) / u32(g->k);
-    if (rules && E == 8 && digests && fused_waves <= 2048 && ps >= 32768)
+    // 1 MiB stripes take it at any grid size (C3 8,192 x 1 MiB: 4.94 ->
+    // 5.13 TB/s), 256 KiB ones only in small grids (C4 16,384 x 256 KiB:
+    // nibble-table fused 5.00, warp-specialised 4.76; profiles/r02/ab_c3_c4_enc.txt)
+    if (rules && E == 8 && digests && ps >= 32768 && (fused_waves <= 2048 || ps >= 131072))
         return nkfs_ws_encode(g, ids, digests, 4, false, st);
     // Nibble tables free LDS (N8K5: 25 -> 11 KB per wave, the occupancy
     // limit) at twice the lookups: a win where the grid offers more waves

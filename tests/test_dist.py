@@ -1,6 +1,8 @@
 """Multi-rank plumbing of bench.py on CPU (gloo, world size 2): weak-scaling
-stripe partition, max-over-ranks timing, digest all-gather.  The GPU run uses
-the same functions over RCCL (backend "nccl") with one process per GPU."""
+stripe partition, byte-balanced ragged (C5) partition, max-over-ranks timing,
+digest all-gather (uneven per-rank counts included) and rank 0's cross-rank
+digest check.  The GPU run uses the same functions over RCCL (backend
+"nccl") with one process per GPU."""
 import os
 import socket
 
@@ -39,14 +41,38 @@ def _worker(rank, world, port, q):
         g = r * per + s
         mine += [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
     local = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in mine], dtype=torch.int64)
+
+    def expect(rr, s):
+        g = rr * per + s
+        return [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
+
     gathered = bench.gather_digests(local, dev)
-    ok = bench.check_rank_digests(gathered, per, B, n, k, samples=per) if r == 0 else None
+    ok = bench.check_rank_digests(gathered, n, expect, samples=per) if r == 0 else None
+    bad_local = local.clone()
     if r == 1:  # a wrong digest on rank 1 is caught by rank 0
-        local[5] += 1
-    bad = bench.gather_digests(local, dev)
-    nok = bench.check_rank_digests(bad, per, B, n, k, samples=per) if r == 0 else None
+        bad_local[5] += 1
+    bad = bench.gather_digests(bad_local, dev)
+    nok = bench.check_rank_digests(bad, n, expect, samples=per) if r == 0 else None
+    # C5: byte-balanced ranges of one global ragged batch, uneven stripe
+    # counts per rank; each rank's digests of its own range, checked by rank 0
+    n5, k5 = 3, 2
+    sizes = synth.mixed_sizes(2 * 9, (40, 700, 5000))
+    ranges = bench.byte_balanced_ranges(sizes, w)
+    lo, hi = ranges[r]
+    d5 = []
+    for g in range(lo, hi):
+        d5 += [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, int(sizes[g])), n5, k5, synth.stripe_ids(g, n5))]
+    t5 = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in d5], dtype=torch.int64)
+
+    def expect5(rr, s):
+        g = ranges[rr][0] + s
+        return [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, int(sizes[g])), n5, k5, synth.stripe_ids(g, n5))]
+
+    g5 = bench.gather_digests(t5, dev)
+    ok5 = bench.check_rank_digests(g5, n5, expect5, samples=100) if r == 0 else None
+    counts5 = [len(x) // n5 for x in g5]
     bench.barrier()
-    q.put((r, w, local.numel(), first, count, t, xs, ok, nok))
+    q.put((r, w, local.numel(), first, count, t, xs, ok, nok, ok5, counts5, ranges))
     dist.destroy_process_group()
 
 
@@ -62,10 +88,11 @@ def test_two_rank_gloo():
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    for r, (rank, world, nd, first, count, t, xs, ok, nok) in enumerate(res):
+    for r, (rank, world, nd, first, count, t, xs, ok, nok, ok5, counts5, ranges) in enumerate(res):
         assert (rank, world, nd) == (r, 2, 16)
         if r == 0:
-            assert ok == 2 and nok == -1
+            assert ok == 2 and nok == -1 and ok5 == 2
+        assert counts5 == [hi - lo for lo, hi in ranges] and ranges[0][0] == 0 and ranges[-1][1] == 18
         assert (first, count) == (r * 65536, 65536)  # disjoint stripe ranges, fixed per-GPU work
         assert t == 2.0                              # max over ranks
         assert xs == [0xF000_0000_0000_0000, 0xF000_0000_0000_0001]
@@ -79,14 +106,14 @@ def test_single_rank_defaults(monkeypatch):
     assert bench.gather_digest_xor(7, torch.device("cpu")) == [7]
 
 
-def test_strong_scaling_partition():
-    """--strong-total: a fixed total split evenly, disjoint and covering
-    (8,192 x 1 MiB over 1/2/4/8 GPUs); weak by default."""
-    assert bench.per_rank_stripes(2048, 0, 8) == 2048
+def test_byte_balanced_ranges():
+    """C5 partition: contiguous, disjoint, covering ranges
+    whose user bytes differ by at most one stripe's size."""
+    from nkfs_amd import synth
+    sizes = synth.mixed_sizes(11520 * 4)
     for world in (1, 2, 4, 8):
-        per = bench.per_rank_stripes(2048, 8192, world)
-        ranges = [bench.stripe_range(r, per) for r in range(world)]
-        covered = [s for first, count in ranges for s in range(first, first + count)]
-        assert covered == list(range(8192))
-    with pytest.raises(SystemExit):
-        bench.per_rank_stripes(2048, 8192, 3)
+        ranges = bench.byte_balanced_ranges(sizes, world)
+        assert ranges[0][0] == 0 and ranges[-1][1] == len(sizes)
+        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+        per = [int(sizes[lo:hi].sum()) for lo, hi in ranges]
+        assert max(per) - min(per) <= 2 * int(sizes.max())

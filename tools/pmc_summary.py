@@ -49,6 +49,10 @@ for k, cs in sorted(out.items(), key=lambda kv: -sum(kv[1].values())):
                              (f"{kind}_write_size", w)):
                 rec[key] = rec.get(key, 0) + int(val)
 if a.json and a.config:
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import CONFIGS
+    rec["stripes"] = CONFIGS[a.config][0]  # bench.py uses the figure only for this batch size
     doc = {}
     if os.path.exists(a.json):
         doc = json.load(open(a.json))
