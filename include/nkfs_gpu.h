@@ -31,10 +31,27 @@ extern "C" {
 #endif
 
 /* Initialise the GPU side without the reference's self test (nk8_init runs
- * this plus the test).  device < 0: env NKFS_DEVICE or the current device. */
+ * this plus the test).  device < 0: env NKFS_DEVICE or the current device.
+ * That device is the library's device: the compatibility entry points
+ * (nkfs_crt.h) run there. */
 int nkfs_gpu_init(int device);
 /* 1 when the library has a usable GPU context. */
 int nkfs_gpu_ready(void);
+/* The library's device (-1 before init) and the number of visible devices. */
+int nkfs_gpu_device(void);
+int nkfs_gpu_count(void);
+
+/* Multi-GPU (stripes are independent).  Batched device
+ * calls run on the device of the stream they are given (each device's
+ * tables are set up on first use).  The host-memory entry points below
+ * split every batch into byte-balanced contiguous stripe ranges over the
+ * device lanes set here -- one host thread and three streams per lane, no
+ * data exchanged between lanes; an entry may repeat (two lanes on one
+ * device).  count 0 = the library's device only (the default).  Returns
+ * -ENODEV for a device that does not exist. */
+int nkfs_gpu_set_devices(const int *devices, int count);
+/* Current lanes into devices[0..max); returns their number. */
+int nkfs_gpu_get_devices(int *devices, int max);
 
 /* Kernel choice and launch shape of the batched entry points.  The library
  * starts with the measured defaults; tools and tests replace
@@ -51,6 +68,7 @@ struct nkfs_tune {
 	int enc_nib;          /* walk encoder, n > 4: nibble product tables (-1 auto, 0, 1) */
 	int enc_units;        /* walk encoder: 1,024-row units per chunk (0 auto, 1, 2; n <= 4 only) */
 	int size_order;       /* ragged batches run largest stripe first (0/1) */
+	int enc_prefetch;     /* walk encoder: chunks of loads in flight ahead of the one encoded (1, 2) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields */
@@ -123,6 +141,15 @@ int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch,
 			   const uint64_t *d_expect, uint64_t *d_badmask,
 			   void *stream);
 
+/* nkfs_nk8_decode_ragged with the part check of nkfs_nk8_decode_verify
+ * (d_expect[s*n_slots + j] = XXH64 of slot j; status -EIO + d_badmask). */
+int nkfs_nk8_decode_ragged_verify(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots,
+				  const uint8_t *d_ids, const uint8_t *d_avail, int navail, int k,
+				  uint8_t *d_blocks, const uint64_t *d_block_off,
+				  const uint32_t *d_block_size, uint32_t max_block_size,
+				  uint32_t nstripes, void *d_work, int32_t *d_status,
+				  const uint64_t *d_expect, uint64_t *d_badmask, void *stream);
+
 /* XXH64 of `count` messages d_base + d_off[i], d_len[i] bytes each
  * (d_off[i] a multiple of 8) -- the batched form of csum_* for the core's
  * per-64 KiB-block integrity sums (core/dio.c:26-37). */
@@ -154,27 +181,41 @@ int nkfs_pages_dsum_batch(const uint8_t *const *d_pages,
 			  uint32_t count, uint32_t page_size,
 			  uint64_t *d_dsums, void *stream);
 
+/* ---- host-memory entry points ----
+ * The path's real ends: PUT = socket -> core/upages.c page buffers ->
+ * device -> parts; GET = parts -> device -> page buffers.  Every call is
+ * synchronous (returns when the outputs are in host memory) and cuts the
+ * batch into sub-batches of about `chunk_bytes` of blocks (0 = 32 MiB) that
+ * flow through three streams per device lane, so H2D, kernels and D2H of
+ * consecutive sub-batches overlap.  Contiguous host buffers that the HIP
+ * runtime does not know as pinned are registered for the call (reference
+ * counted: concurrent calls may share a buffer); page lists are gathered
+ * into / scattered from pinned staging.  Only defined outputs are written:
+ * part bytes between a part's size and its pitch are unspecified, bytes
+ * between stripes and the blocks of stripes that fail to decode
+ * (-EINVAL: fewer than k distinct ids) keep the caller's contents.
+ * The calling thread is left with the library's device current. */
+
+/* Pin a host range for the library's DMA once (e.g. a server's page pool),
+ * so per-call pinning becomes a reference bump.  -EEXIST when the runtime
+ * already knows the range as pinned (nothing to do). */
+int nkfs_host_register(void *p, size_t bytes);
+int nkfs_host_unregister(void *p);
+
 /* Host-memory form of nkfs_nk8_encode: blocks, ids, parts and digests in
- * host memory (the path's real entry: socket -> page buffers -> device,
- * SURVEY.md §8(f) row 2).  The batch is cut into sub-batches of about
- * `chunk_bytes` of user data that flow through two streams, so the H2D of
- * one sub-batch, the fused encode+XXH64 of the previous and the D2H of its
- * parts overlap.  Host buffers that are not already pinned are registered
- * (hipHostRegister) for the duration of the call.  Synchronous: returns
- * when parts and digests are in host memory.  chunk_bytes 0 = 32 MiB. */
+ * host memory. */
 int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch,
 			 uint32_t block_size, uint32_t nstripes, int n, int k,
 			 const uint8_t *h_ids, uint8_t *h_parts,
 			 uint64_t part_pitch, uint64_t *h_digests,
 			 uint64_t chunk_bytes);
 
-/* Host-memory form of nkfs_nk8_encode_ragged (the C5 mixed batch from page
- * buffers): stripe s is h_block_size[s] bytes at h_blocks + h_block_off[s],
- * part i goes to h_parts + h_part_off[s] + i*nkfs_part_pitch(
- * h_block_size[s], k), digests to h_digests[s*n + i].  Offsets must be
- * non-decreasing in s (-EINVAL otherwise).  Consecutive stripes of about
- * chunk_bytes (0 = 32 MiB) flow through the GPU as one sub-batch each,
- * H2D / kernels / D2H overlapped as nkfs_nk8_encode_host.  Synchronous. */
+/* Host-memory form of nkfs_nk8_encode_ragged (the C5 mixed batch):
+ * stripe s is h_block_size[s] bytes at h_blocks + h_block_off[s], part i
+ * goes to h_parts + h_part_off[s] + i*nkfs_part_pitch(h_block_size[s], k)
+ * (h_part_off[s] a multiple of 16), digests to h_digests[s*n + i].  Blocks
+ * and part ranges must be in increasing order without overlap (gaps are
+ * allowed and left untouched); -EINVAL otherwise. */
 int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks,
 				const uint64_t *h_block_off,
 				const uint32_t *h_block_size,
@@ -182,6 +223,49 @@ int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks,
 				int n, int k, const uint8_t *h_ids,
 				uint8_t *h_parts, const uint64_t *h_part_off,
 				uint64_t *h_digests, uint64_t chunk_bytes);
+
+/* PUT from page lists (core/upages.c:91-122: struct nkfs_pages, an array
+ * of page pointers): block s is the first h_block_size[s] bytes of pages
+ * h_pages[h_first_page[s]], h_pages[h_first_page[s] + 1], ... (page_size
+ * bytes each).  Parts and digests as nkfs_nk8_encode_ragged_host. */
+int nkfs_nk8_encode_pages(const uint8_t *const *h_pages, uint32_t page_size,
+			  const uint64_t *h_first_page, const uint32_t *h_block_size,
+			  uint32_t max_block_size, uint32_t nstripes, int n, int k,
+			  const uint8_t *h_ids, uint8_t *h_parts,
+			  const uint64_t *h_part_off, uint64_t *h_digests,
+			  uint64_t chunk_bytes);
+
+/* GET: nkfs_nk8_decode from host memory.  Stripe s's n_slots part slots
+ * are at h_parts + (s*n_slots + j)*part_pitch; every slot travels over
+ * PCIe, so pass the parts you hold (e.g. the k survivors, n_slots = k).
+ * Selection, status (h_status may be NULL) as nkfs_nk8_decode; with
+ * h_expect != NULL the part check of nkfs_nk8_decode_verify is fused in
+ * (status -EIO, h_badmask may be NULL). */
+int nkfs_nk8_decode_host(const uint8_t *h_parts, uint64_t part_pitch, int n_slots,
+			 const uint8_t *h_ids, const uint8_t *h_avail, int navail, int k,
+			 uint32_t block_size, uint8_t *h_blocks, uint64_t block_pitch,
+			 uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect,
+			 uint64_t *h_badmask, uint64_t chunk_bytes);
+
+/* GET of a ragged batch: layout of nkfs_nk8_encode_ragged_host with
+ * n_slots slots per stripe at h_parts + h_part_off[s] + j*pitch(B_s). */
+int nkfs_nk8_decode_ragged_host(const uint8_t *h_parts, const uint64_t *h_part_off,
+				int n_slots, const uint8_t *h_ids, const uint8_t *h_avail,
+				int navail, int k, uint8_t *h_blocks,
+				const uint64_t *h_block_off, const uint32_t *h_block_size,
+				uint32_t max_block_size, uint32_t nstripes, int32_t *h_status,
+				const uint64_t *h_expect, uint64_t *h_badmask,
+				uint64_t chunk_bytes);
+
+/* GET into page lists (the read side of core/net.c:228-265): parts as
+ * nkfs_nk8_decode_ragged_host, block s written to its pages as
+ * nkfs_nk8_encode_pages reads them. */
+int nkfs_nk8_decode_pages(const uint8_t *h_parts, const uint64_t *h_part_off, int n_slots,
+			  const uint8_t *h_ids, const uint8_t *h_avail, int navail, int k,
+			  uint8_t *const *h_pages, uint32_t page_size,
+			  const uint64_t *h_first_page, const uint32_t *h_block_size,
+			  uint32_t max_block_size, uint32_t nstripes, int32_t *h_status,
+			  const uint64_t *h_expect, uint64_t *h_badmask, uint64_t chunk_bytes);
 
 /* Fill a uniform batch with the seeded counter-based splitmix64 stripes of
  * nkfs_amd/synth.py (bench / test input synthesis on the device). */

@@ -30,7 +30,7 @@ vp = C.c_void_p
 class Tune(C.Structure):
     """struct nkfs_tune (include/nkfs_gpu.h): kernel choice and launch shape."""
     _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
-                                       "dec_units", "enc_nib", "enc_units", "size_order")]
+                                       "dec_units", "enc_nib", "enc_units", "size_order", "enc_prefetch")]
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4}
@@ -77,6 +77,22 @@ _SIGS = {
     "nkfs_pages_dsum_batch": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp]),
     "nkfs_nk8_encode_host": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int, vp, vp,
                                        C.c_uint64, vp, C.c_uint64]),
+    "nkfs_nk8_decode_ragged_verify": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32,
+                                                C.c_uint32, vp, vp, vp, vp, vp]),
+    "nkfs_nk8_encode_pages": (C.c_int, [vp, C.c_uint32, vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, vp, vp,
+                                        vp, vp, C.c_uint64]),
+    "nkfs_nk8_decode_host": (C.c_int, [vp, C.c_uint64, C.c_int, vp, vp, C.c_int, C.c_int, C.c_uint32, vp,
+                                       C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64]),
+    "nkfs_nk8_decode_ragged_host": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32,
+                                              C.c_uint32, vp, vp, vp, C.c_uint64]),
+    "nkfs_nk8_decode_pages": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, C.c_uint32, vp, vp,
+                                        C.c_uint32, C.c_uint32, vp, vp, vp, C.c_uint64]),
+    "nkfs_host_register": (C.c_int, [vp, C.c_size_t]),
+    "nkfs_host_unregister": (C.c_int, [vp]),
+    "nkfs_gpu_device": (C.c_int, []),
+    "nkfs_gpu_count": (C.c_int, []),
+    "nkfs_gpu_set_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
+    "nkfs_gpu_get_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "nkfs_synth_blocks": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, vp]),
     "nkfs_dev_alloc": (vp, [C.c_size_t]),
     "nkfs_dev_free": (None, [vp]),

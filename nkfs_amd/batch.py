@@ -11,6 +11,8 @@ Layout of a uniform batch (see include/nkfs_gpu.h):
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from ._lib import check, lib
@@ -200,6 +202,88 @@ def encode_ragged_host(blocks, block_off, block_sizes, n: int, k: int, ids, part
     check(lib().nkfs_nk8_encode_ragged_host(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), mb, nstripes, n, k,
                                             t[3].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), _ptr(dg),
                                             chunk_bytes), "nkfs_nk8_encode_ragged_host")
+
+
+def _host(x, dt, nm):
+    t = torch.as_tensor(x)
+    if t.is_cuda or t.dtype != dt or not t.is_contiguous():
+        raise ValueError(f"{nm}: contiguous {dt} host array")
+    return t
+
+
+def encode_pages(pages, page_size: int, first_page, block_sizes, n: int, k: int, ids, parts, part_off,
+                 digests=None, max_block_size: int | None = None, chunk_bytes: int = 0):
+    """PUT from page lists (nkfs_nk8_encode_pages): pages int64 [npages]
+    host page addresses, block s = first block_sizes[s] bytes of pages
+    first_page[s], first_page[s]+1, ...; parts/digests written in place."""
+    pg, fp, sz = _host(pages, torch.int64, "pages"), _host(first_page, torch.int64, "first_page"), \
+        _host(block_sizes, torch.int32, "block_sizes")
+    it, pt, po = _host(ids, U8, "ids"), _host(parts, U8, "parts"), _host(part_off, torch.int64, "part_off")
+    dg = None if digests is None else _host(digests, torch.int64, "digests")
+    mb = int(sz.max()) if max_block_size is None and sz.numel() else (max_block_size or 1)
+    return lib().nkfs_nk8_encode_pages(pg.data_ptr(), page_size, fp.data_ptr(), sz.data_ptr(), mb, sz.numel(), n, k,
+                                       it.data_ptr(), pt.data_ptr(), po.data_ptr(), _ptr(dg), chunk_bytes)
+
+
+def decode_host(parts, part_pitch: int, n_slots: int, ids, avail, navail: int, k: int, block_size: int, blocks,
+                block_pitch: int | None = None, status=None, expect=None, badmask=None, chunk_bytes: int = 0):
+    """GET from host memory (nkfs_nk8_decode_host); blocks written in place.
+    Returns the library's return code."""
+    pt, it, av, bt = _host(parts, U8, "parts"), _host(ids, U8, "ids"), _host(avail, U8, "avail"), \
+        _host(blocks, U8, "blocks")
+    st = None if status is None else _host(status, torch.int32, "status")
+    ex = None if expect is None else _host(expect, torch.int64, "expect")
+    bm = None if badmask is None else _host(badmask, torch.int64, "badmask")
+    nstripes = it.numel() // n_slots
+    return lib().nkfs_nk8_decode_host(pt.data_ptr(), part_pitch, n_slots, it.data_ptr(), av.data_ptr(), navail, k,
+                                      block_size, bt.data_ptr(), block_pitch or block_size, nstripes, _ptr(st),
+                                      _ptr(ex), _ptr(bm), chunk_bytes)
+
+
+def decode_ragged_host(parts, part_off, n_slots: int, ids, avail, navail: int, k: int, blocks, block_off,
+                       block_sizes, status=None, expect=None, badmask=None, max_block_size: int | None = None,
+                       chunk_bytes: int = 0):
+    """GET of a ragged batch from host memory (nkfs_nk8_decode_ragged_host)."""
+    pt, po, it, av = _host(parts, U8, "parts"), _host(part_off, torch.int64, "part_off"), _host(ids, U8, "ids"), \
+        _host(avail, U8, "avail")
+    bt, bo, sz = _host(blocks, U8, "blocks"), _host(block_off, torch.int64, "block_off"), \
+        _host(block_sizes, torch.int32, "block_sizes")
+    st = None if status is None else _host(status, torch.int32, "status")
+    ex = None if expect is None else _host(expect, torch.int64, "expect")
+    bm = None if badmask is None else _host(badmask, torch.int64, "badmask")
+    mb = int(sz.max()) if max_block_size is None and sz.numel() else (max_block_size or 1)
+    return lib().nkfs_nk8_decode_ragged_host(pt.data_ptr(), po.data_ptr(), n_slots, it.data_ptr(), av.data_ptr(),
+                                             navail, k, bt.data_ptr(), bo.data_ptr(), sz.data_ptr(), mb, sz.numel(),
+                                             _ptr(st), _ptr(ex), _ptr(bm), chunk_bytes)
+
+
+def decode_pages(parts, part_off, n_slots: int, ids, avail, navail: int, k: int, pages, page_size: int, first_page,
+                 block_sizes, status=None, expect=None, badmask=None, max_block_size: int | None = None,
+                 chunk_bytes: int = 0):
+    """GET into page lists (nkfs_nk8_decode_pages)."""
+    pt, po, it, av = _host(parts, U8, "parts"), _host(part_off, torch.int64, "part_off"), _host(ids, U8, "ids"), \
+        _host(avail, U8, "avail")
+    pg, fp, sz = _host(pages, torch.int64, "pages"), _host(first_page, torch.int64, "first_page"), \
+        _host(block_sizes, torch.int32, "block_sizes")
+    st = None if status is None else _host(status, torch.int32, "status")
+    ex = None if expect is None else _host(expect, torch.int64, "expect")
+    bm = None if badmask is None else _host(badmask, torch.int64, "badmask")
+    mb = int(sz.max()) if max_block_size is None and sz.numel() else (max_block_size or 1)
+    return lib().nkfs_nk8_decode_pages(pt.data_ptr(), po.data_ptr(), n_slots, it.data_ptr(), av.data_ptr(), navail,
+                                       k, pg.data_ptr(), page_size, fp.data_ptr(), sz.data_ptr(), mb, sz.numel(),
+                                       _ptr(st), _ptr(ex), _ptr(bm), chunk_bytes)
+
+
+def set_devices(devices) -> int:
+    """nkfs_gpu_set_devices: device lanes of the host-memory entry points."""
+    arr = (C.c_int * max(1, len(devices)))(*devices)
+    return lib().nkfs_gpu_set_devices(arr, len(devices))
+
+
+def get_devices() -> list[int]:
+    arr = (C.c_int * 16)()
+    n = lib().nkfs_gpu_get_devices(arr, 16)
+    return list(arr[:n])
 
 
 def xxh64_batch(base: torch.Tensor, off: torch.Tensor, lens: torch.Tensor, seed: int = 0, stream=None):

@@ -65,37 +65,60 @@ XXH_errorcode XXH64_reset(XXH64_state_t *state_in, unsigned long long seed)
 	return XXH_OK;
 }
 
-/* Fold `nst` stripes: first the buffered one (if `lead`), then the caller's
- * bytes, into s->v on the device. */
+/* Stripes per device pass: the input streams through bounded pinned and
+ * device scratch (8 MiB + the state), so any length hashes without a
+ * device allocation of its size. */
+#define FOLD_CHUNK (8u << 20)
+
+/* Fold the buffered stripe (if `lead`) and `nst_input` stripes of the
+ * caller's bytes into s->v on the device: state + stripes are staged in
+ * pinned memory and go over in one copy per chunk; the accumulators stay
+ * on the device between chunks and come back once. */
 static int fold_stripes(struct xstate *s, const uint8_t *lead, const uint8_t *input, uint64_t nst_input)
 {
 	struct nkfs_ctx *c = nkfs_ctx_get();
 	if (!c)
 		return -EIO;
 	int err;
-	uint64_t lead_bytes = lead ? 32 : 0;
-	uint64_t bytes = 32 + lead_bytes + nst_input * 32;
+	const uint64_t total = (lead ? 1 : 0) + nst_input;  /* stripes */
+	const uint64_t first = total * 32 < FOLD_CHUNK ? total * 32 : FOLD_CHUNK;
 	void *dv, *hv;
-	if ((err = nkfs_ctx_dev(c, bytes, &dv)) || (err = nkfs_ctx_host(c, 64, &hv)))
+	if ((err = nkfs_ctx_dev(c, 64 + first, &dv)) || (err = nkfs_ctx_host(c, 64 + first, &hv)))
 		goto out;
-	uint8_t *d = dv;
-	memcpy(hv, s->v, 32);
-	if (lead)
-		memcpy((uint8_t *)hv + 32, lead, 32);
-	if (hipMemcpyAsync(d, hv, 32 + lead_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-	    (nst_input && hipMemcpyAsync(d + 32 + lead_bytes, input, nst_input * 32, hipMemcpyHostToDevice,
-					 c->stream) != hipSuccess)) {
-		err = -EIO;
-		goto out;
+	uint8_t *d = dv, *h = hv;
+	memcpy(h, s->v, 32);
+	uint64_t done = 0;  /* input stripes consumed */
+	for (int pass = 0; done < nst_input || (pass == 0 && lead); pass++) {
+		uint64_t off = pass == 0 ? 32 : 0; /* pass 0 carries the state */
+		uint64_t room = (FOLD_CHUNK - (pass == 0 && lead ? 32 : 0)) / 32;
+		uint64_t take = nst_input - done < room ? nst_input - done : room;
+		uint8_t *hp = h + 32;
+		if (pass == 0 && lead) {
+			memcpy(hp, lead, 32);
+			hp += 32;
+		}
+		if (pass) /* the previous pass's copy must be done before the staging is reused */
+			if (hipStreamSynchronize(c->stream) != hipSuccess) {
+				err = -EIO;
+				goto out;
+			}
+		memcpy(hp, input + done * 32, take * 32);
+		const uint64_t nst = take + (pass == 0 && lead ? 1 : 0);
+		if (hipMemcpyAsync(d + 32 - off, h + 32 - off, off + nst * 32, hipMemcpyHostToDevice, c->stream) !=
+		    hipSuccess) {
+			err = -EIO;
+			goto out;
+		}
+		if ((err = nkfs_launch_xxh64_stripes((uint64_t *)d, d + 32, nst, c->stream)))
+			goto out;
+		done += take;
 	}
-	if ((err = nkfs_launch_xxh64_stripes((uint64_t *)d, d + 32, (lead_bytes + nst_input * 32) / 32, c->stream)))
-		goto out;
-	if (hipMemcpyAsync(hv, d, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+	if (hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
 	    hipStreamSynchronize(c->stream) != hipSuccess) {
 		err = -EIO;
 		goto out;
 	}
-	memcpy(s->v, hv, 32);
+	memcpy(s->v, h, 32);
 out:
 	nkfs_ctx_put(c);
 	return err;

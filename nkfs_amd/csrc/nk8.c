@@ -90,7 +90,10 @@ static int gen_part_ids(uint8_t *ids, int n)
 
 static uint64_t round16(uint64_t v) { return (v + 15) & ~(uint64_t)15; }
 
-/* Encode one block on the GPU with explicit ids into host part buffers. */
+/* Encode one block on the GPU with explicit ids into host part buffers.
+ * Block and ids go over in one copy from pinned staging, the n parts come
+ * back in one copy (the per-call fixed cost is two copies, one launch and
+ * one stream sync). */
 static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8_t *ids, uint8_t **parts)
 {
 	struct nkfs_ctx *c = nkfs_ctx_get();
@@ -99,20 +102,23 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 	int err;
 	uint32_t ps = nkfs_part_size(B, k);
 	uint64_t pitch = nkfs_part_pitch(B, k);
-	uint64_t off_parts = round16(B), off_ids = off_parts + pitch * (uint64_t)n;
-	void *dv;
-	if ((err = nkfs_ctx_dev(c, off_ids + round16((uint64_t)n), &dv)))
+	uint64_t off_ids = round16(B), off_parts = off_ids + round16((uint64_t)n);
+	uint64_t in_bytes = off_parts, parts_bytes = pitch * (uint64_t)n;
+	void *dv, *hv;
+	if ((err = nkfs_ctx_dev(c, off_parts + parts_bytes, &dv)) ||
+	    (err = nkfs_ctx_host(c, in_bytes > parts_bytes ? in_bytes : parts_bytes, &hv)))
 		goto out;
-	uint8_t *d = dv;
-	HIPGO(hipMemcpyAsync(d, block, B, hipMemcpyHostToDevice, c->stream));
-	HIPGO(hipMemcpyAsync(d + off_ids, ids, (size_t)n, hipMemcpyHostToDevice, c->stream));
+	uint8_t *d = dv, *h = hv;
+	memcpy(h, block, B);
+	memcpy(h + off_ids, ids, (size_t)n);
+	HIPGO(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
 	struct nkfs_geom g = { d, round16(B), B, NULL, NULL, d + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0 };
 	if ((err = nkfs_launch_encode(&g, d + off_ids, NULL, nkfs_gf(), c->stream)))
 		goto out;
-	for (int i = 0; i < n; i++)
-		HIPGO(hipMemcpyAsync(parts[i], d + off_parts + pitch * (uint64_t)i, ps, hipMemcpyDeviceToHost,
-				     c->stream));
+	HIPGO(hipMemcpyAsync(h, d + off_parts, parts_bytes, hipMemcpyDeviceToHost, c->stream));
 	HIPGO(hipStreamSynchronize(c->stream));
+	for (int i = 0; i < n; i++)
+		memcpy(parts[i], h + pitch * (uint64_t)i, ps);
 	err = 0;
 out:
 	nkfs_ctx_put(c);
@@ -177,33 +183,37 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 	int err;
 	uint32_t ps = nkfs_part_size(block_size, k);
 	uint64_t pitch = nkfs_part_pitch(block_size, k);
+	/* device and pinned staging share one layout for the inputs:
+	 * parts | ids | avail, one H2D; block | status come back in one D2H */
 	uint64_t off_parts = 0;
 	uint64_t off_ids = off_parts + pitch * (uint64_t)k;
 	uint64_t off_avail = off_ids + 256;
-	uint64_t off_status = off_avail + 256;
-	uint64_t off_work = off_status + 16;
-	uint64_t off_block = off_work + round16(nkfs_decode_work_bytes(1, k));
+	uint64_t off_work = off_avail + 256;
+	uint64_t off_status = off_work + round16(nkfs_decode_work_bytes(1, k));
+	uint64_t off_block = off_status + 16;
+	uint64_t in_bytes = off_work, out_bytes = 16 + round16(block_size);
 	void *dv, *hv;
-	if ((err = nkfs_ctx_dev(c, off_block + round16(block_size), &dv)) || (err = nkfs_ctx_host(c, 528, &hv)))
+	if ((err = nkfs_ctx_dev(c, off_block + round16(block_size), &dv)) ||
+	    (err = nkfs_ctx_host(c, in_bytes > out_bytes ? in_bytes : out_bytes, &hv)))
 		goto out;
 	uint8_t *d = dv, *h = hv;
 	for (int c2 = 0; c2 < k; c2++) {
-		HIPGO(hipMemcpyAsync(d + off_parts + pitch * (uint64_t)c2, parts[sel[c2]], ps, hipMemcpyHostToDevice,
-				     c->stream));
-		h[c2] = ids[sel[c2]];
-		h[256 + c2] = (uint8_t)c2;
+		memcpy(h + off_parts + pitch * (uint64_t)c2, parts[sel[c2]], ps);
+		h[off_ids + c2] = ids[sel[c2]];
+		h[off_avail + c2] = (uint8_t)c2;
 	}
-	HIPGO(hipMemcpyAsync(d + off_ids, h, 512, hipMemcpyHostToDevice, c->stream));
+	HIPGO(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
 	struct nkfs_geom g = { d + off_block, round16(block_size), block_size, NULL, NULL, d + off_parts, pitch,
 			       NULL, 1, k, k, NULL, 0, 0 };
 	if ((err = nkfs_launch_decode(&g, k, d + off_ids, d + off_avail, k, d + off_work,
 				      (int32_t *)(d + off_status), nkfs_gf(), c->stream, NULL, NULL)))
 		goto out;
-	HIPGO(hipMemcpyAsync(block, d + off_block, block_size, hipMemcpyDeviceToHost, c->stream));
-	int32_t st = 0;
-	HIPGO(hipMemcpyAsync(h + 512, d + off_status, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+	HIPGO(hipMemcpyAsync(h, d + off_status, 16 + block_size, hipMemcpyDeviceToHost, c->stream));
 	HIPGO(hipStreamSynchronize(c->stream));
-	memcpy(&st, h + 512, sizeof(st));
+	int32_t st;
+	memcpy(&st, h, sizeof(st));
+	if (!st)
+		memcpy(block, h + 16, block_size);
 	err = st;
 out:
 	nkfs_ctx_put(c);

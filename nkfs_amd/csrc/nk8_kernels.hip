@@ -130,25 +130,25 @@ __global__ __launch_bounds__(256) void k_encode_generic(nkfs_geom g, const u8 *i
     for (int i = threadIdx.x; i < g.n; i += blockDim.x)
         lid[i] = L.log[ids[u64(s) * g.n + i]];
     __syncthreads();
-    const u32 j = blockIdx.y * blockDim.x + threadIdx.x;
-    if (j >= v.ps)
-        return;
-    const u64 row = u64(j) * g.k;
     const int kk = g.k;
-    for (int i = 0; i < g.n; ++i) {
-        const int li = lid[i];
-        int la = 0;  // log of ids[i]^m
-        u8 acc = 0;
-        for (int m = 0; m < kk; ++m) {
-            const u64 pos = row + m;
-            const u8 x = pos < v.B ? v.blk[pos] : u8(0);
-            if (x)
-                acc ^= L.exp[la + L.log[x]];
-            la += li;
-            if (la >= 255)
-                la -= 255;
+    // rows grid-stride over grid.y (capped at 65,535 by the launcher)
+    for (u32 j = blockIdx.y * blockDim.x + threadIdx.x; j < v.ps; j += gridDim.y * blockDim.x) {
+        const u64 row = u64(j) * kk;
+        for (int i = 0; i < g.n; ++i) {
+            const int li = lid[i];
+            int la = 0;  // log of ids[i]^m
+            u8 acc = 0;
+            for (int m = 0; m < kk; ++m) {
+                const u64 pos = row + m;
+                const u8 x = pos < v.B ? v.blk[pos] : u8(0);
+                if (x)
+                    acc ^= L.exp[la + L.log[x]];
+                la += li;
+                if (la >= 255)
+                    la -= 255;
+            }
+            v.parts[u64(i) * v.pitch + j] = acc;
         }
-        v.parts[u64(i) * v.pitch + j] = acc;
     }
 }
 
@@ -215,17 +215,42 @@ __global__ __launch_bounds__(256) void k_xxh64_batch(const u8 *base, const u64 *
 
 // Streaming XXH64 for the csum_*/XXH64_* compatibility entry points: fold
 // `nst` whole 32-byte stripes into the four accumulators of one state
-// (crt/xxhash.c:788-821), then (separately) finish.
-__global__ void k_xxh64_stripes(u64 *state_v, const u8 *data, u64 nst)
+// (crt/xxhash.c:788-821), then (separately) finish.  One message is one
+// serial chain per accumulator, so four lanes do the rounds; the whole wave
+// streams the input: every lane loads 32 B of the next 2 KiB piece
+// (coalesced) while lanes 0-3 fold the current piece from LDS, so no round
+// waits on a global load.
+__global__ __launch_bounds__(64) void k_xxh64_stripes(u64 *state_v, const u8 *data, u64 nst)
 {
-    const int a = threadIdx.x;
-    if (a >= 4)
-        return;
-    u64 acc = state_v[a];
-    const u64 *w = reinterpret_cast<const u64 *>(data) + a;
-    for (u64 r = 0; r < nst; ++r)
-        acc = xxh_round(acc, w[4 * r]);
-    state_v[a] = acc;
+    __shared__ u64 buf[2][64 * 4 + 4];  // piece = 64 stripes; +4: stagger the two halves
+    const int li = threadIdx.x;
+    const int a = li & 3;
+    u64 acc = li < 4 ? state_v[a] : 0;
+    const u64 *src = reinterpret_cast<const u64 *>(data);
+    const u64 pieces = (nst + 63) / 64;
+    u64 w[4] = {0, 0, 0, 0};
+    auto load = [&](u64 p) {
+        const u64 st = p * 64 + u64(li);  // this lane's stripe
+        if (p < pieces && st < nst)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                w[q] = src[st * 4 + q];
+    };
+    load(0);
+    for (u64 p = 0; p < pieces; ++p) {
+        u64 *b = buf[p & 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            b[li * 4 + q] = w[q];
+        __syncthreads();
+        load(p + 1);  // in flight under this piece's rounds
+        const u64 cnt = nst - p * 64 < 64 ? nst - p * 64 : 64;
+        if (li < 4)
+            for (u64 r = 0; r < cnt; ++r)
+                acc = xxh_round(acc, b[r * 4 + a]);
+    }
+    if (li < 4)
+        state_v[a] = acc;
 }
 
 __global__ void k_xxh64_finish(u64 *out, const u64 *state_v, u64 total_len, u64 seed, const u8 *tail,
@@ -324,21 +349,20 @@ __global__ __launch_bounds__(256) void k_decode_generic(nkfs_geom g, int n_slots
         return;
     const int k = g.k;
     const StripeView v = stripe_view(g, s);  // g.n = n_slots; blocks = the output
-    const u32 j = blockIdx.y * blockDim.x + threadIdx.x;
-    if (j >= v.ps)
-        return;
     const u8 *wk = work + u64(s) * u64(k + k * k);
     u8 *out = const_cast<u8 *>(v.blk);
-    const u64 row = u64(j) * k;
-    for (int m = 0; m < k; ++m) {
-        if (row + m >= v.B)
-            break;
-        u8 acc = 0;
-        for (int c = 0; c < k; ++c) {
-            const u8 pv = v.parts[u64(wk[c]) * v.pitch + j];
-            acc ^= gf_mul(L, pv, wk[k + c * k + m]);
+    for (u32 j = blockIdx.y * blockDim.x + threadIdx.x; j < v.ps; j += gridDim.y * blockDim.x) {
+        const u64 row = u64(j) * k;
+        for (int m = 0; m < k; ++m) {
+            if (row + m >= v.B)
+                break;
+            u8 acc = 0;
+            for (int c = 0; c < k; ++c) {
+                const u8 pv = v.parts[u64(wk[c]) * v.pitch + j];
+                acc ^= gf_mul(L, pv, wk[k + c * k + m]);
+            }
+            out[row + m] = acc;
         }
-        out[row + m] = acc;
     }
 }
 
@@ -471,6 +495,14 @@ static int launch_ok(void)
     return e == hipSuccess ? 0 : -EIO;
 }
 
+// grid.y of the general kernels: 256 rows per block, at most 65,535 blocks
+// (the kernels grid-stride over the rest: parts beyond ~16 MiB)
+static u32 row_blocks(u32 ps)
+{
+    const u32 b = (ps + 255) / 256;
+    return b < 1 ? 1 : b > 65535 ? 65535 : b;
+}
+
 static u32 max_part_size(const nkfs_geom *g, u32 max_block)
 {
     return part_size_of(g->block_sizes ? max_block : g->block_size, g->k);
@@ -517,14 +549,29 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids,
                                  void *work, int32_t *status, const void *gf, int units, int waves, hipStream_t st);
 
 // Fast-path encoder choice (n <= 8, k <= 8), struct nkfs_tune.enc_kernel:
-// AUTO = the fused / warp-specialised shape rules for uniform batches (the
-// walk encoder measured equal on N8K5 shapes and slower on N4K2 4 KiB,
-// DESIGN.md §4) and the walk encoder for ragged ones (one wave per stripe in
-// size order; the fused kernel would pair unequal stripes in one wave).
+// AUTO = the walk encoder for ragged batches (one wave per stripe in size
+// order; the fused kernel would pair unequal stripes in one wave) and for
+// mid-size uniform N8 shapes (walk_by_rule), else the fused /
+// warp-specialised shape rules (the walk encoder is slower on N4K2 4 KiB,
+// where one stripe is one chunk).
+static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
+{
+    // uniform n > 4 batches of 32-128 KiB parts on grids beyond 2,048 fused
+    // waves (C4: 16,384 x 256 KiB): the walk encoder, 4.75-4.93 -> 4.89-5.14
+    // TB/s across boxes (profiles/r02/ab_walk_encoder.txt); 1 MiB stripes stay
+    // on the warp-specialised kernel (C3: walk 4.99-5.03, ws 5.08-5.15)
+    if (g->block_sizes || !digests || g->n <= 4)
+        return 0;
+    const u32 ps = (g->block_size + u32(g->k) - 1) / u32(g->k);
+    return ps >= 32768 && ps < 131072 && (g->nstripes + 1) / 2 > 2048;
+}
+
 static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStream_t st)
 {
     const nkfs_tune &t = nkfs_g_tune;
-    const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel : g->block_sizes ? NKFS_ENC_WALK : NKFS_ENC_AUTO;
+    const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
+                     : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
+                                                                  : NKFS_ENC_AUTO;
     if (kern == NKFS_ENC_WALK) {
         // two 1,024-row units per chunk for n <= 4 (a 4 KiB N4K2 stripe is one chunk)
         const int units = g->n <= 4 ? (t.enc_units ? t.enc_units : 2) : 1;
@@ -553,7 +600,7 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     if (rc != -ENOSYS)
         return rc;
     const u32 ps = max_part_size(g, g->block_size);
-    dim3 grid(g->nstripes, (ps + 255) / 256);
+    dim3 grid(g->nstripes, row_blocks(ps));
     hipLaunchKernelGGL(k_encode_generic, grid, dim3(256), 0, st, *g, ids, (const GfTables *)gf);
     if ((rc = launch_ok()))
         return rc;
@@ -608,7 +655,7 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     if (rc)
         return rc;
     const u32 ps = part_size_of(g->block_size, g->k);
-    dim3 grid(g->nstripes, (ps + 255) / 256);
+    dim3 grid(g->nstripes, row_blocks(ps));
     hipLaunchKernelGGL(k_decode_generic, grid, dim3(256), 0, st, *g, n_slots, (const u8 *)work,
                        (const int32_t *)status, (const GfTables *)gf);
     if ((rc = launch_ok()) || !expect)

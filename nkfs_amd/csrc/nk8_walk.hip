@@ -127,7 +127,11 @@ __device__ inline void load_rows(u32 (&d)[4 * K], const Stripe &v, u64 off, bool
 
 }  // namespace
 
-constexpr u32 OOB = 0x80000000u;  // buffer offset past every num_records: load 0 / store dropped
+// Buffer offset `off` (< 2^31) when `live`, else past every num_records
+// (the load reads 0 / the store is dropped), as plain
+// arithmetic: a select here tempts the compiler to branch around each
+// load/store, which splits the step's straight-line block
+__device__ inline u32 live_off(bool live, u32 off) { return off | (u32(!live) << 31); }
 
 __device__ inline __amdgpu_buffer_rsrc_t rsrc(const void *base, u32 bytes)
 {
@@ -137,7 +141,7 @@ __device__ inline __amdgpu_buffer_rsrc_t rsrc(const void *base, u32 bytes)
 // Persistent walk.  Wave w walks stripes w, w + grid, w + 2*grid, ...
 // (per_wave of them; ragged batches: exactly one, g.order applied), each in
 // chunks of R = 1024*U rows; every (stripe, chunk) is one task and step t
-//   1. loads task t+1 (the next chunk, or the next stripe's first),
+//   1. loads task t+P (P = 1 or 2 tasks of loads in flight ahead),
 //   2. folds task t-1's parts into the XXH64 chains (finishing a stripe's
 //      digests after its last chunk),
 //   3. encodes task t (tables rebuilt when it starts a stripe), stores it and
@@ -148,7 +152,7 @@ __device__ inline __amdgpu_buffer_rsrc_t rsrc(const void *base, u32 bytes)
 // in flight under steps 2-3 (the wait before task t's data covers only what
 // was issued before it).  Two register sets alternate; step 0 is peeled so
 // the loop is entered in the same state it loops back in.
-template <int K, int E, int U, bool HASH, bool NIB, bool RAGGED>
+template <int K, int E, int U, int P, bool HASH, bool NIB, bool RAGGED>
 __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *ids, u64 *digests, u32 per_wave)
 {
     constexpr int R = 1024 * U;                // rows per chunk
@@ -207,14 +211,16 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
         const bool ok = task_ok(t, j);
         // num_records rounded up to a dword: the buffer unit range-checks whole
         // dwords (a dword straddling num_records reads 0); bytes past B in it
-        // are masked below (a dword never crosses a page, so it is mapped)
-        const __amdgpu_buffer_rsrc_t r = rsrc(ok ? blk_of(stripe_of(j)) : g.blocks, (B + 3u) & ~3u);
+        // are masked below (a dword never crosses a page, so it is mapped).
+        // The base is formed even for a task past the end: its offsets are
+        // all out of range, so nothing is read.
+        const __amdgpu_buffer_rsrc_t r = rsrc(blk_of(stripe_of(j)), (B + 3u) & ~3u);
         const u32 cb = c * u32(R * K);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int q = 0; q < K; ++q) {
-                const u32 off = ok ? cb + u32((u * 1024 + 16 * li) * K + 16 * q) : OOB;
+                const u32 off = live_off(ok, cb + u32((u * 1024 + 16 * li) * K + 16 * q));
                 const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
                 x[u][4 * q] = v.x;
                 x[u][4 * q + 1] = v.y;
@@ -232,63 +238,17 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
     u64 acc = xxh_acc_init(ha, 0);
 
     auto step = [&](Buf &cur, Buf &nxt, u32 t) {
-        // task cursors: t-1 (fold), t (encode), t+1 (load); uniform shapes
+        // task cursors: t-1 (fold), t (encode), t+P (load); uniform shapes
         const u32 je = t / nch, ce = t - je * nch;
-        const u32 jl = (t + 1) / nch, cl = (t + 1) - jl * nch;
-        load_task(nxt, t + 1, jl, cl);
-
-        // fold task t-1 (predicated, straight-line: the compiler interleaves
-        // the serial rounds with this step's table lookups)
+        const u32 jl = (t + P) / nch, cl = (t + P) - jl * nch;
+        load_task(nxt, t + P, jl, cl);
         const u32 jf = t >= 1 ? (t - 1) / nch : 0, cf = t >= 1 ? (t - 1) - jf * nch : 0;
         const bool fok = HASH && t >= 1 && task_ok(t - 1, jf);
-        if constexpr (HASH) {
-            const u32 rbase = fok ? cf * RPC : nst;
-#pragma unroll
-            for (int r = 0; r < RPC; ++r) {
-                const u64 w = *reinterpret_cast<const u64 *>(hsrc + 32 * r);
-                const u64 nx = xxh_round(acc, w);
-                acc = rbase + r < nst ? nx : acc;
-            }
-        }
-        if constexpr (HASH) {
-            // a stripe's last chunk was folded: its digests (merge, length,
-            // tail still in the exchange, avalanche); one digest store per
-            // step, dropped unless a stripe finished here
-            u64 dval = 0;
-            const bool fin = fok && cf == nch - 1;
-            if (fin) {
-                const int base = li & ~3;
-                const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
-                const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
-                u64 h = ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
-                h += ps;
-                u64 tw[4] = {0, 0, 0, 0};
-                if (left) {
-                    const u64 *src = reinterpret_cast<const u64 *>(xbuf + (hi < E ? hi : 0) * SP + toff);
-#pragma unroll
-                    for (int w = 0; w < 4; ++w)
-                        tw[w] = src[w];
-                }
-                dval = xxh_tail_regs(h, tw, left);
-                acc = xxh_acc_init(ha, 0);
-            }
-            const u32 doff = fin && hi < n && ha == 0 ? (stripe_of(jf) * u32(n) + u32(hi)) * 8u : OOB;
-            const v2u dv = {u32(dval), u32(dval >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(dv, drs, doff, 0, 0);
-        }
-
+        const bool fin = fok && cf == nch - 1;
         const bool eok = task_ok(t, je);
-        u32 out[U][E][4];
-        // defined on every path, so the stores below compile to one straight
-        // run (undefined data on the !eok path invites the compiler to
-        // split them into branches, each with its own s_waitcnt)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < E; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    out[u][i][q] = 0;
+
+        // wave-uniform, rare: the tables of a stripe that starts here, and
+        // the zero padding of a stripe's last 16-byte piece
         if (eok) {
             if (ce == 0) {
                 // packed product tables T_m, m = 1..K-1, of the stripe starting here
@@ -341,94 +301,189 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
                         cur[u][q] &= keep >= 4 ? 0xFFFFFFFFu : (1u << (8 * keep)) - 1u;
                     }
             }
+        }
+
+        // ---- one straight-line block: fold task t-1 (serial XXH64 rounds
+        // from words read out of the exchange up front), encode task t
+        // (table lookups in flight a row group ahead), the exchange write,
+        // the stores.  Work past the end (!eok) computes on zeros and its
+        // stores are dropped, so no branch splits the block.
+        u64 wv[HASH ? RPC : 1];
+        u64 tw[4] = {0, 0, 0, 0};
+        if constexpr (HASH) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
+            for (int r = 0; r < RPC; ++r)
+                wv[r] = *reinterpret_cast<const u64 *>(hsrc + 32 * r);
+            // the tail words of a part whose last chunk this is (read
+            // before the exchange is overwritten; used only when fin)
+            const u64 *tsrc = reinterpret_cast<const u64 *>(xbuf + (hi < E ? hi : 0) * SP + toff);
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                tw[w] = tsrc[w];
+        }
+        u32 out[U][E][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (!NIB) {
+                // byte tables: the 4(K-1) lookups of a group of 4 rows are
+                // issued together, one group ahead of the XORs that use
+                // them, so a wave keeps up to 8(K-1) LDS reads in flight
+                // instead of waiting on every row's K-1
+                u32 ent[2][4][K - 1][W];
+                auto look = [&](int q, u32 (&e)[4][K - 1][W]) {
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                        for (int m = 1; m < K; ++m) {
+                            const int p = (4 * q + rr) * K + m;
+                            const u32 byte = (cur[u][p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                            const u8 *ep = tbl + (m - 1) * TB + byte * E;
+                            if constexpr (E == 8) {
+                                const uint2 tt = *reinterpret_cast<const uint2 *>(ep);
+                                e[rr][m - 1][0] = tt.x;
+                                e[rr][m - 1][W - 1] = tt.y;
+                            } else {
+                                e[rr][m - 1][0] = *reinterpret_cast<const u32 *>(ep);
+                            }
+                        }
+                };
+                look(0, ent[0]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    if (q < 3)
+                        look(q + 1, ent[(q + 1) & 1]);
                     u32 row[4][W];
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
                         const int p0 = (4 * q + rr) * K;
                         const u32 rep = __builtin_amdgcn_perm(0u, cur[u][p0 >> 2], 0x01010101u * u32(p0 & 3));
 #pragma unroll
-                        for (int w = 0; w < W; ++w)
-                            row[rr][w] = rep;
+                        for (int w = 0; w < W; ++w) {
+                            u32 x = rep;
 #pragma unroll
-                        for (int m = 1; m < K; ++m) {
-                            const int p = p0 + m;
-                            const u32 byte = (cur[u][p >> 2] >> (8 * (p & 3))) & 0xFFu;
-                            const u8 *tb = tbl + (m - 1) * TB;
-                            if constexpr (NIB) {
-                                const u8 *e0 = tb + (byte & 15u) * E;
-                                const u8 *e1 = tb + (16u + (byte >> 4)) * E;
-                                if constexpr (E == 8) {
-                                    const uint2 t0 = *reinterpret_cast<const uint2 *>(e0);
-                                    const uint2 t1 = *reinterpret_cast<const uint2 *>(e1);
-                                    row[rr][0] ^= t0.x ^ t1.x;
-                                    row[rr][1] ^= t0.y ^ t1.y;
-                                } else {
-                                    row[rr][0] ^= *reinterpret_cast<const u32 *>(e0) ^ *reinterpret_cast<const u32 *>(e1);
-                                }
-                            } else {
-                                const u8 *e = tb + byte * E;
-                                if constexpr (E == 8) {
-                                    const uint2 tt = *reinterpret_cast<const uint2 *>(e);
-                                    row[rr][0] ^= tt.x;
-                                    row[rr][1] ^= tt.y;
-                                } else {
-                                    row[rr][0] ^= *reinterpret_cast<const u32 *>(e);
-                                }
-                            }
+                            for (int m = 1; m < K; ++m)
+                                x ^= ent[q & 1][rr][m - 1][w];
+                            row[rr][w] = x;
                         }
                     }
 #pragma unroll
                     for (int w = 0; w < W; ++w)
-                        transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[u][4 * w][q], out[u][4 * w + 1][q],
-                                   out[u][4 * w + 2][q], out[u][4 * w + 3][q]);
+                        transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[u][4 * w][q],
+                                   out[u][4 * w + 1][q], out[u][4 * w + 2][q], out[u][4 * w + 3][q]);
                 }
-                if constexpr (HASH)
+            } else {
+                // nibble tables: T_m[x] = L_m[x & 15] ^ H_m[x >> 4], two
+                // conflict-free lookups per byte; a row group's lookups are
+                // issued before its XORs
 #pragma unroll
-                    for (int i = 0; i < E; ++i)
-                        *reinterpret_cast<uint4 *>(xbuf + i * SP + u * 1024 + 16 * li) =
-                            make_uint4(out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]);
+                for (int q = 0; q < 4; ++q) {
+                    u32 e[4][K - 1][2][W];
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                        for (int m = 1; m < K; ++m) {
+                            const int p = (4 * q + rr) * K + m;
+                            const u32 byte = (cur[u][p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                            const u8 *tb = tbl + (m - 1) * TB;
+                            const u8 *e0 = tb + (byte & 15u) * E;
+                            const u8 *e1 = tb + (16u + (byte >> 4)) * E;
+                            if constexpr (E == 8) {
+                                const uint2 t0 = *reinterpret_cast<const uint2 *>(e0);
+                                const uint2 t1 = *reinterpret_cast<const uint2 *>(e1);
+                                e[rr][m - 1][0][0] = t0.x;
+                                e[rr][m - 1][0][W - 1] = t0.y;
+                                e[rr][m - 1][1][0] = t1.x;
+                                e[rr][m - 1][1][W - 1] = t1.y;
+                            } else {
+                                e[rr][m - 1][0][0] = *reinterpret_cast<const u32 *>(e0);
+                                e[rr][m - 1][1][0] = *reinterpret_cast<const u32 *>(e1);
+                            }
+                        }
+                    u32 row[4][W];
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int p0 = (4 * q + rr) * K;
+                        const u32 rep = __builtin_amdgcn_perm(0u, cur[u][p0 >> 2], 0x01010101u * u32(p0 & 3));
+#pragma unroll
+                        for (int w = 0; w < W; ++w) {
+                            u32 x = rep;
+#pragma unroll
+                            for (int m = 1; m < K; ++m)
+                                x ^= e[rr][m - 1][0][w] ^ e[rr][m - 1][1][w];
+                            row[rr][w] = x;
+                        }
+                    }
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[u][4 * w][q],
+                                   out[u][4 * w + 1][q], out[u][4 * w + 2][q], out[u][4 * w + 3][q]);
+                }
             }
         }
+
         if constexpr (HASH) {
-            // this task's parts into the exchange, after the fold and the tail read
-            if (eok)
+            const u32 rbase = fok ? cf * RPC : nst;
 #pragma unroll
-                for (int u = 0; u < U; ++u)
+            for (int r = 0; r < RPC; ++r) {
+                const u64 nx = xxh_round(acc, wv[r]);
+                acc = rbase + r < nst ? nx : acc;
+            }
+            // this task's parts into the exchange, after the reads above
 #pragma unroll
-                    for (int i = 0; i < E; ++i)
-                        *reinterpret_cast<uint4 *>(xbuf + i * SP + u * 1024 + 16 * li) =
-                            make_uint4(out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int i = 0; i < E; ++i)
+                    *reinterpret_cast<uint4 *>(xbuf + i * SP + u * 1024 + 16 * li) =
+                        make_uint4(out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]);
         }
         // stores: n parts x U units of 1 KiB runs; dropped where not live
-        const __amdgpu_buffer_rsrc_t prs = rsrc(eok ? par_of(stripe_of(je)) : g.parts, pbytes);
+        const __amdgpu_buffer_rsrc_t prs = rsrc(par_of(stripe_of(je)), pbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const u32 r0 = ce * u32(R) + u32(u * 1024 + 16 * li);
 #pragma unroll
             for (int i = 0; i < E; ++i) {
-                const u32 off = eok && i < n && r0 < ps ? u32(i) * u32(ppitch) + r0 : OOB;
+                const u32 off = live_off(eok & (i < n) & (r0 < ps), u32(i) * u32(ppitch) + r0);
                 const v4u v = {out[u][i][0], out[u][i][1], out[u][i][2], out[u][i][3]};
                 __builtin_amdgcn_raw_buffer_store_b128(v, prs, off, 0, 0);
             }
         }
+        if constexpr (HASH) {
+            // a stripe's last chunk was folded: its digests (merge, length,
+            // tail, avalanche); one digest store per step, dropped unless a
+            // stripe finished here
+            u64 dval = 0;
+            if (fin) {
+                const int base = li & ~3;
+                const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+                const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+                u64 h = ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+                h += ps;
+                dval = xxh_tail_regs(h, tw, left);
+                acc = xxh_acc_init(ha, 0);
+            }
+            const u32 doff = live_off(fin & (hi < n) & (ha == 0), (stripe_of(jf) * u32(n) + u32(hi)) * 8u);
+            const v2u dv = {u32(dval), u32(dval >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(dv, drs, doff, 0, 0);
+        }
         __builtin_amdgcn_wave_barrier();
     };
 
-    u32 da[U][4 * K], db[U][4 * K];
-    load_task(da, 0, 0, 0);
+    // P + 1 register sets in rotation: step t encodes set t % (P+1) and
+    // loads task t + P into set (t + P) % (P+1)
+    u32 xb[P + 1][U][4 * K];
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+        load_task(xb[p], u32(p), u32(p) / nch, u32(p) % nch);
     const u32 last = HASH ? ntask : ntask - 1;  // step ntask only folds
-    step(da, db, 0);
-    for (u32 t = 1;;) {
-        if (t > last)
-            break;
-        step(db, da, t++);
-        if (t > last)
-            break;
-        step(da, db, t++);
+    step(xb[0], xb[P], 0);
+    for (u32 t = 1; t <= last;) {
+#pragma unroll
+        for (int q = 1; q <= P + 1; ++q) {
+            if (t > last)
+                break;
+            step(xb[q % (P + 1)], xb[(q + P) % (P + 1)], t++);
+        }
     }
 }
 
@@ -654,20 +709,21 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
 
 // ----------------------------------------------------------------- launchers
 
-template <int K, int E, int U, bool HASH, bool NIB>
+template <int K, int E, int U, int P, bool HASH, bool NIB>
 static void launch_walk_kk(hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
 {
     // uniform batches: persistent grid of the resident waves, walking stripes
     // grid-stride (at most 64 stripes per wave: their ids are staged in LDS);
     // ragged: one wave per stripe
     if (g.block_sizes) {
-        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, HASH, NIB, true>),
+        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, P, HASH, NIB, true>),
                                          waves);
-        hipLaunchKernelGGL((k_encode_walk<K, E, U, HASH, NIB, true>), dim3(g.nstripes), dim3(64), sh.pad, st, g, ids,
-                           dig, 1u);
+        hipLaunchKernelGGL((k_encode_walk<K, E, U, P, HASH, NIB, true>), dim3(g.nstripes), dim3(64), sh.pad, st, g,
+                           ids, dig, 1u);
         return;
     }
-    const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, HASH, NIB, false>), waves);
+    const Shape sh =
+        occupancy_shape(reinterpret_cast<const void *>(&k_encode_walk<K, E, U, P, HASH, NIB, false>), waves);
     const u32 cap = u32(cus) * u32(sh.per_cu);
     u32 grid = g.nstripes < cap ? g.nstripes : cap;
     u32 per_wave = (g.nstripes + grid - 1) / grid;
@@ -675,23 +731,33 @@ static void launch_walk_kk(hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
         per_wave = 64;
         grid = (g.nstripes + 63) / 64;
     }
-    hipLaunchKernelGGL((k_encode_walk<K, E, U, HASH, NIB, false>), dim3(grid), dim3(64), sh.pad, st, g, ids, dig,
+    hipLaunchKernelGGL((k_encode_walk<K, E, U, P, HASH, NIB, false>), dim3(grid), dim3(64), sh.pad, st, g, ids, dig,
                        per_wave);
 }
 
+template <int E, int U, int P, bool HASH, bool NIB>
+static int launch_walk_kp(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
+{
+    switch (k) {
+    case 2: launch_walk_kk<2, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 3: launch_walk_kk<3, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 4: launch_walk_kk<4, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 5: launch_walk_kk<5, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 6: launch_walk_kk<6, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 7: launch_walk_kk<7, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    case 8: launch_walk_kk<8, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
+    default: return -ENOSYS;
+    }
+}
+
+// prefetch depth 2 only for the byte-table forms (nibble tables keep P = 1)
 template <int E, int U, bool HASH, bool NIB>
 static int launch_walk_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
 {
-    switch (k) {
-    case 2: launch_walk_kk<2, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 3: launch_walk_kk<3, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 4: launch_walk_kk<4, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 5: launch_walk_kk<5, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 6: launch_walk_kk<6, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 7: launch_walk_kk<7, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 8: launch_walk_kk<8, E, U, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    default: return -ENOSYS;
-    }
+    if constexpr (!NIB)
+        if (nkfs_g_tune.enc_prefetch >= 2)
+            return launch_walk_kp<E, U, 2, HASH, NIB>(k, st, g, ids, dig, waves, cus);
+    return launch_walk_kp<E, U, 1, HASH, NIB>(k, st, g, ids, dig, waves, cus);
 }
 
 // Walk encoder for n <= 8, k <= 8 (uniform or ragged; g->order honoured).

@@ -1,10 +1,34 @@
 /*
- * pipeline.c -- host-memory entry points: sub-batches streamed through the
- * GPU on two streams so that PCIe H2D, the fused kernels and PCIe D2H
- * overlap (the reference's path starts and ends in host memory: client
- * socket -> core/upages.c page buffers -> block device).
+ * pipeline.c -- host-memory entry points: the path's real ends.  The
+ * reference's PUT starts at the client socket, lands in core/upages.c page
+ * buffers (an array of 4 KiB pages, core/upages.c:91-122) and ends on the
+ * block device; its GET runs the other way (core/net.c:228-265,
+ * client/lib/client.c:183-235).  Here a host batch --
+ * contiguous blocks, a packed ragged batch or page lists -- streams through
+ * the GPU in sub-batches:
+ *
+ *   encode:  blocks H2D -> fused encode + XXH64 -> parts and digests D2H
+ *   decode:  parts H2D  -> K x K inverse + rebuild (+ part XXH64 verify)
+ *            -> status D2H, then the blocks of the stripes that decoded D2H
+ *
+ * Each sub-batch rides one of three pooled per-call contexts (stream, device
+ * scratch, pinned scratch), so the H2D of one sub-batch, the kernels of the
+ * next and the D2H of a third overlap.  Page lists are gathered into /
+ * scattered from pinned staging by the host (a page pointer is caller
+ * memory the GPU never dereferences); contiguous caller buffers go straight
+ * over DMA (pinned for the call when the runtime does not know them, with a
+ * reference-counted registry so concurrent calls on the same buffer never
+ * unpin under each other).  Only bytes the API defines as outputs are
+ * written back: part runs of abutting stripes, blocks of stripes that
+ * decoded (gaps and failed stripes keep the caller's bytes).
+ *
+ * With several device lanes (nkfs_gpu_set_devices) a batch is cut into
+ * byte-balanced contiguous stripe ranges, one host thread and one device
+ * lane each, no data exchanged between them (stripes are independent,
+ * SURVEY.md §8(e)).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -15,32 +39,704 @@
 #include "nkfs_internal.h"
 #include "runtime.h"
 
-/* pin a caller buffer for the call unless the runtime already knows it */
-static int pin(const void *p, size_t bytes, int *registered)
+/* ------------------------------------------------------ pinned registry */
+
+struct pin_ent {
+	uintptr_t base;
+	size_t bytes;
+	int refs;
+	struct pin_ent *next;
+};
+static pthread_mutex_t g_pin_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct pin_ent *g_pins;
+
+/* Pin [p, p+bytes) for a call: memory the runtime already knows as pinned
+ * (hipHostMalloc, torch pinned memory, a range someone else registered)
+ * needs nothing; a range inside one this registry holds takes a reference;
+ * anything else is registered here with one reference.  *held = the entry
+ * to release (NULL when nothing was taken). */
+static int pin_take(const void *p, size_t bytes, struct pin_ent **held)
 {
-	*registered = 0;
+	*held = NULL;
 	if (!p || !bytes)
 		return 0;
+	const uintptr_t a = (uintptr_t)p;
+	int rc = 0;
+	pthread_mutex_lock(&g_pin_lock);
+	for (struct pin_ent *e = g_pins; e; e = e->next)
+		if (a >= e->base && a + bytes <= e->base + e->bytes) {
+			e->refs++;
+			*held = e;
+			goto out;
+		}
 	hipPointerAttribute_t attr;
-	if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost)
-		return 0;
-	(void)hipGetLastError();
-	hipError_t e = hipHostRegister((void *)p, bytes, hipHostRegisterDefault);
-	if (e == hipErrorHostMemoryAlreadyRegistered) {
-		(void)hipGetLastError();
-		return 0;
+	if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) {
+		/* pinned by its owner; a range that only starts inside such an
+		 * allocation is the caller's contract (it must stay pinned) */
+		goto out;
 	}
-	if (e != hipSuccess)
-		return nkfs_hip_fail("hipHostRegister", (int)e);
-	*registered = 1;
+	(void)hipGetLastError();
+	struct pin_ent *e = malloc(sizeof(*e));
+	if (!e) {
+		rc = -ENOMEM;
+		goto out;
+	}
+	hipError_t he = hipHostRegister((void *)p, bytes, hipHostRegisterPortable);
+	if (he != hipSuccess) {
+		(void)hipGetLastError();
+		free(e);
+		/* partly overlapping someone else's registration: refuse rather
+		 * than DMA from memory that may be unpinned mid-copy */
+		rc = he == hipErrorHostMemoryAlreadyRegistered ? -EBUSY : nkfs_hip_fail("hipHostRegister", (int)he);
+		goto out;
+	}
+	e->base = a;
+	e->bytes = bytes;
+	e->refs = 1;
+	e->next = g_pins;
+	g_pins = e;
+	*held = e;
+out:
+	pthread_mutex_unlock(&g_pin_lock);
+	return rc;
+}
+
+static void pin_drop(struct pin_ent *e)
+{
+	if (!e)
+		return;
+	pthread_mutex_lock(&g_pin_lock);
+	if (--e->refs == 0) {
+		for (struct pin_ent **pp = &g_pins; *pp; pp = &(*pp)->next)
+			if (*pp == e) {
+				*pp = e->next;
+				break;
+			}
+		hipHostUnregister((void *)e->base);
+		free(e);
+	}
+	pthread_mutex_unlock(&g_pin_lock);
+}
+
+int nkfs_host_register(void *p, size_t bytes)
+{
+	struct pin_ent *e;
+	if (!p || !bytes)
+		return -EINVAL;
+	int rc = pin_take(p, bytes, &e);
+	if (!rc && !e)
+		return -EEXIST; /* pinned by its owner: nothing to hold */
+	return rc;
+}
+
+int nkfs_host_unregister(void *p)
+{
+	pthread_mutex_lock(&g_pin_lock);
+	struct pin_ent *e = g_pins;
+	while (e && e->base != (uintptr_t)p)
+		e = e->next;
+	pthread_mutex_unlock(&g_pin_lock);
+	if (!e)
+		return -ENOENT;
+	pin_drop(e);
 	return 0;
 }
 
-/* Three sub-batches in flight (H2D of one, kernels of another, D2H of a
- * third); each rides a pooled context (its stream and growable device
- * scratch are reused across calls, so a call creates no streams and
- * allocates no device memory once warm). */
+/* ------------------------------------------------------- batch description */
+
+enum { HP_ENC = 0, HP_DEC = 1 };
+
+struct hp {
+	int dir, n, k, n_slots, navail;
+	uint32_t nstripes, max_block;
+	/* uniform geometry (sizes == NULL) */
+	uint32_t block_size;
+	uint64_t block_pitch, part_pitch;
+	/* ragged geometry */
+	const uint32_t *sizes;
+	const uint64_t *boff, *poff;
+	/* block side: contiguous, or a page list */
+	uint8_t *blocks;
+	uint8_t *const *pages;
+	const uint64_t *first_page;
+	uint32_t page_size;
+	/* part side: contiguous */
+	uint8_t *parts;
+	const uint8_t *ids, *avail;
+	uint64_t *digests;
+	const uint64_t *expect;
+	uint64_t *badmask;
+	int32_t *status;
+	uint64_t chunk;
+};
+
+static uint32_t hp_B(const struct hp *h, uint32_t s) { return h->sizes ? h->sizes[s] : h->block_size; }
+
+static int hp_slots(const struct hp *h) { return h->dir == HP_ENC ? h->n : h->n_slots; }
+
+static uint64_t hp_ppitch(const struct hp *h, uint32_t s)
+{
+	return h->sizes ? nkfs_part_pitch(h->sizes[s], h->k) : h->part_pitch;
+}
+
+/* byte offsets of stripe s's block / part slots in the caller's buffers */
+static uint64_t hp_bofs(const struct hp *h, uint32_t s)
+{
+	if (h->pages)
+		return 0; /* page lists: no contiguous block side */
+	return h->sizes ? h->boff[s] : (uint64_t)s * h->block_pitch;
+}
+
+static uint64_t hp_pofs(const struct hp *h, uint32_t s)
+{
+	return h->sizes ? h->poff[s] : (uint64_t)s * (uint64_t)hp_slots(h) * h->part_pitch;
+}
+
+static uint64_t hp_pspan(const struct hp *h, uint32_t s) { return (uint64_t)hp_slots(h) * hp_ppitch(h, s); }
+
+static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
+
+/* ------------------------------------------------------------ sub-batches */
+
 #define NSTREAM 3
+
+/* Device / pinned scratch layout of one sub-batch of at most `cnt` stripes
+ * (offsets into the context buffers). */
+struct lay {
+	uint64_t d_blk, d_parts, d_boff, d_poff, d_sz, d_ids, d_avail, d_dig, d_status, d_bad, d_work, d_total;
+	uint64_t h_boff, h_poff, h_sz, h_ids, h_avail, h_dig, h_status, h_bad, h_stage, h_total;
+};
+
+struct sub {
+	uint32_t s0, s1;     /* stripes [s0, s1) */
+	uint64_t blo, bhi;   /* caller block byte range (contiguous side) */
+	uint64_t plo, phi;   /* caller part byte range */
+	int live;            /* issued, not yet retired */
+	int copied;          /* decode: block D2H issued */
+	hipEvent_t ev;       /* decode: status ready */
+};
+
+struct lane {
+	const struct hp *h;
+	int dev;
+	uint32_t s0, s1;
+	int rc;
+};
+
+/* Next sub-batch starting at s0: consecutive stripes with at most
+ * h->chunk bytes of blocks (at least one). */
+static uint32_t sub_end(const struct hp *h, uint32_t s0, uint32_t lim)
+{
+	uint64_t bytes = hp_B(h, s0);
+	uint32_t s1 = s0 + 1;
+	while (s1 < lim && bytes + hp_B(h, s1) <= h->chunk)
+		bytes += hp_B(h, s1++);
+	return s1;
+}
+
+static void sub_ranges(const struct hp *h, struct sub *u)
+{
+	u->blo = hp_bofs(h, u->s0);
+	u->plo = hp_pofs(h, u->s0);
+	u->bhi = u->blo;
+	u->phi = u->plo;
+	for (uint32_t s = u->s0; s < u->s1; s++) {
+		const uint64_t be = hp_bofs(h, s) + hp_B(h, s), pe = hp_pofs(h, s) + hp_pspan(h, s);
+		u->bhi = be > u->bhi ? be : u->bhi;
+		u->phi = pe > u->phi ? pe : u->phi;
+	}
+}
+
+static int hp_paged(const struct hp *h) { return h->pages != NULL; }
+
+/* device bytes of the blocks of [s0, s1) */
+static uint64_t dev_block_bytes(const struct hp *h, const struct sub *u)
+{
+	if (!hp_paged(h))
+		return u->bhi - u->blo;
+	uint64_t t = 0;
+	for (uint32_t s = u->s0; s < u->s1; s++)
+		t += align256(hp_B(h, s));
+	return t;
+}
+
+static void layout(const struct hp *h, uint32_t cnt, uint64_t blk_bytes, uint64_t part_bytes, struct lay *L)
+{
+	const uint64_t nsl = (uint64_t)hp_slots(h);
+	uint64_t o = 0;
+	L->d_blk = o;
+	o += align256(blk_bytes);
+	L->d_parts = o;
+	o += align256(part_bytes);
+	L->d_boff = o;
+	o += align256(cnt * 8ull);
+	L->d_poff = o;
+	o += align256(cnt * 8ull);
+	L->d_sz = o;
+	o += align256(cnt * 4ull);
+	L->d_ids = o;
+	o += align256(cnt * nsl);
+	L->d_avail = o;
+	o += align256(cnt * (uint64_t)(h->navail > 0 ? h->navail : 1));
+	L->d_dig = o;
+	o += align256(cnt * nsl * 8);
+	L->d_status = o;
+	o += align256(cnt * 4ull);
+	L->d_bad = o;
+	o += align256(cnt * 8ull);
+	L->d_work = o;
+	o += align256(nkfs_decode_work_bytes(cnt, h->k));
+	L->d_total = o;
+
+	o = 0;
+	L->h_boff = o;
+	o += align256(cnt * 8ull);
+	L->h_poff = o;
+	o += align256(cnt * 8ull);
+	L->h_sz = o;
+	o += align256(cnt * 4ull);
+	L->h_ids = o;
+	o += align256(cnt * nsl);
+	L->h_avail = o;
+	o += align256(cnt * (uint64_t)(h->navail > 0 ? h->navail : 1));
+	L->h_dig = o;
+	o += align256(cnt * nsl * 8);
+	L->h_status = o;
+	o += align256(cnt * 4ull);
+	L->h_bad = o;
+	o += align256(cnt * 8ull);
+	L->h_stage = o;
+	o += hp_paged(h) ? align256(blk_bytes) : 0;
+	L->h_total = o;
+}
+
+/* copy block s of a page list into dst (gather) or back (scatter) */
+static void page_copy(const struct hp *h, uint32_t s, uint8_t *buf, int to_pages)
+{
+	const uint32_t B = hp_B(h, s), P = h->page_size;
+	uint8_t *const *pg = h->pages + h->first_page[s];
+	for (uint32_t off = 0, i = 0; off < B; off += P, i++) {
+		const uint32_t len = B - off < P ? B - off : P;
+		if (to_pages)
+			memcpy(pg[i], buf + off, len);
+		else
+			memcpy(buf + off, pg[i], len);
+	}
+}
+
+#define HIPGO(call, what)                                              \
+	do {                                                           \
+		hipError_t e_ = (call);                                \
+		if (e_ != hipSuccess) {                                \
+			rc = nkfs_hip_fail(what, (int)e_);             \
+			goto out;                                      \
+		}                                                      \
+	} while (0)
+
+struct ctxs {
+	struct nkfs_ctx *c;
+	uint8_t *d, *hb;
+	struct lay L;
+	struct sub u;
+};
+
+/* Issue sub-batch u on context x: metadata, H2D, kernels, and for encode
+ * the D2H of parts and digests; for decode the status D2H + event. */
+static int issue(const struct hp *h, struct ctxs *x)
+{
+	int rc = 0;
+	const struct sub *u = &x->u;
+	const uint32_t cnt = u->s1 - u->s0;
+	const struct lay *L = &x->L;
+	hipStream_t st = x->c->stream;
+	uint8_t *d = x->d, *hb = x->hb;
+	const int nsl = hp_slots(h);
+	const int paged = hp_paged(h);
+
+	/* metadata into pinned scratch: ids (+ survivor lists), ragged offsets */
+	memcpy(hb + L->h_ids, h->ids + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl);
+	uint64_t meta_lo = L->h_ids, meta_hi = L->h_ids + (uint64_t)cnt * nsl;
+	if (h->dir == HP_DEC) {
+		memcpy(hb + L->h_avail, h->avail + (uint64_t)u->s0 * h->navail, (size_t)cnt * h->navail);
+		meta_hi = L->h_avail + (uint64_t)cnt * h->navail;
+		if (h->expect) {
+			memcpy(hb + L->h_dig, h->expect + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl * 8);
+			meta_hi = L->h_dig + (uint64_t)cnt * nsl * 8;
+		}
+	}
+	if (h->sizes) {
+		uint64_t *bo = (uint64_t *)(hb + L->h_boff), *po = (uint64_t *)(hb + L->h_poff);
+		uint32_t *sz = (uint32_t *)(hb + L->h_sz);
+		uint64_t packed = 0;
+		for (uint32_t s = u->s0; s < u->s1; s++) {
+			const uint32_t B = hp_B(h, s);
+			if (paged) {
+				bo[s - u->s0] = packed;
+				packed += align256(B);
+			} else {
+				bo[s - u->s0] = h->boff[s] - u->blo;
+			}
+			po[s - u->s0] = h->poff[s] - u->plo;
+			sz[s - u->s0] = B;
+		}
+		meta_lo = L->h_boff;
+	}
+	HIPGO(hipMemcpyAsync(d + L->d_boff + (meta_lo - L->h_boff), hb + meta_lo, meta_hi - meta_lo,
+			     hipMemcpyHostToDevice, st),
+	      "H2D (metadata)");
+
+	/* payload in */
+	if (h->dir == HP_ENC) {
+		if (paged) {
+			uint64_t o = 0;
+			for (uint32_t s = u->s0; s < u->s1; s++) {
+				page_copy(h, s, hb + L->h_stage + o, 0);
+				o += h->sizes ? align256(hp_B(h, s)) : align256(h->block_size);
+			}
+			HIPGO(hipMemcpyAsync(d + L->d_blk, hb + L->h_stage, o, hipMemcpyHostToDevice, st),
+			      "H2D (gathered pages)");
+		} else {
+			HIPGO(hipMemcpyAsync(d + L->d_blk, h->blocks + u->blo, u->bhi - u->blo, hipMemcpyHostToDevice,
+					     st),
+			      "H2D (blocks)");
+		}
+	} else {
+		HIPGO(hipMemcpyAsync(d + L->d_parts, h->parts + u->plo, u->phi - u->plo, hipMemcpyHostToDevice, st),
+		      "H2D (parts)");
+	}
+
+	/* kernels (bases shifted so that the caller-relative offsets land in
+	 * this context's buffers) */
+	const uint64_t dbp = paged ? align256(h->block_size) : h->block_pitch;
+	struct nkfs_geom g;
+	memset(&g, 0, sizeof(g));
+	g.n = nsl;
+	g.k = h->k;
+	g.nstripes = cnt;
+	g.blocks = d + L->d_blk;
+	g.parts = d + L->d_parts;
+	if (h->sizes) {
+		g.block_size = h->max_block;
+		g.block_off = (const uint64_t *)(d + L->d_boff);
+		g.block_sizes = (const uint32_t *)(d + L->d_sz);
+		g.part_off = (const uint64_t *)(d + L->d_poff);
+	} else {
+		g.block_size = h->block_size;
+		g.block_pitch = dbp;
+		g.part_pitch = h->part_pitch;
+	}
+	const void *gf = nkfs_gf_on(x->c->dev);
+	if (!gf) {
+		rc = -ENODEV;
+		goto out;
+	}
+	if (h->dir == HP_ENC) {
+		if ((rc = nkfs_launch_encode(&g, d + L->d_ids, h->digests ? (uint64_t *)(d + L->d_dig) : NULL, gf, st)))
+			goto out;
+		/* parts: runs of abutting stripes only (gaps keep the caller's bytes) */
+		for (uint32_t s = u->s0; s < u->s1;) {
+			uint64_t lo = hp_pofs(h, s), hi = lo + hp_pspan(h, s);
+			uint32_t e = s + 1;
+			while (e < u->s1 && hp_pofs(h, e) == hi)
+				hi += hp_pspan(h, e++);
+			HIPGO(hipMemcpyAsync(h->parts + lo, d + L->d_parts + (lo - u->plo), hi - lo,
+					     hipMemcpyDeviceToHost, st),
+			      "D2H (parts)");
+			s = e;
+		}
+		if (h->digests)
+			HIPGO(hipMemcpyAsync(hb + L->h_dig, d + L->d_dig, (size_t)cnt * nsl * 8, hipMemcpyDeviceToHost, st),
+			      "D2H (digests)");
+	} else {
+		rc = h->expect ? nkfs_launch_decode(&g, nsl, d + L->d_ids, d + L->d_avail, h->navail, d + L->d_work,
+						    (int32_t *)(d + L->d_status), gf, st,
+						    (const uint64_t *)(d + L->d_dig), (uint64_t *)(d + L->d_bad))
+			       : nkfs_launch_decode(&g, nsl, d + L->d_ids, d + L->d_avail, h->navail, d + L->d_work,
+						    (int32_t *)(d + L->d_status), gf, st, NULL, NULL);
+		if (rc)
+			goto out;
+		HIPGO(hipMemcpyAsync(hb + L->h_status, d + L->d_status, (size_t)cnt * 4, hipMemcpyDeviceToHost, st),
+		      "D2H (status)");
+		if (h->badmask)
+			HIPGO(hipMemcpyAsync(hb + L->h_bad, d + L->d_bad, (size_t)cnt * 8, hipMemcpyDeviceToHost, st),
+			      "D2H (badmask)");
+		HIPGO(hipEventRecord(x->u.ev, st), "event record");
+	}
+out:
+	return rc;
+}
+
+/* Decode, second stage: once the status is on the host, copy back the
+ * blocks of the stripes that decoded (a stripe with fewer than k distinct
+ * ids keeps the caller's bytes, as nk8_assemble_block leaves its block). */
+static int copy_blocks(const struct hp *h, struct ctxs *x)
+{
+	int rc = 0;
+	const struct sub *u = &x->u;
+	hipStream_t st = x->c->stream;
+	HIPGO(hipEventSynchronize(u->ev), "status wait");
+	const int32_t *stv = (const int32_t *)(x->hb + x->L.h_status);
+	const int paged = hp_paged(h);
+	uint64_t packed = 0;
+	for (uint32_t s = u->s0; s < u->s1;) {
+		if (stv[s - u->s0] == -EINVAL) {
+			packed += align256(hp_B(h, s));
+			s++;
+			continue;
+		}
+		if (paged) {
+			/* whole sub-batch staging is contiguous: copy runs of good stripes */
+			uint64_t lo = packed, hi = packed + align256(hp_B(h, s));
+			uint32_t e = s + 1;
+			while (e < u->s1 && stv[e - u->s0] != -EINVAL)
+				hi += align256(hp_B(h, e++));
+			HIPGO(hipMemcpyAsync(x->hb + x->L.h_stage + lo, x->d + x->L.d_blk + lo, hi - lo,
+					     hipMemcpyDeviceToHost, st),
+			      "D2H (blocks to staging)");
+			packed = hi;
+			s = e;
+		} else if (!h->sizes && h->block_pitch != h->block_size) {
+			uint32_t e = s + 1;
+			while (e < u->s1 && stv[e - u->s0] != -EINVAL)
+				e++;
+			const uint64_t lo = hp_bofs(h, s);
+			HIPGO(hipMemcpy2DAsync(h->blocks + lo, h->block_pitch, x->d + x->L.d_blk + (lo - u->blo),
+					       h->block_pitch, h->block_size, e - s, hipMemcpyDeviceToHost, st),
+			      "D2H (blocks, pitched)");
+			s = e;
+		} else {
+			uint64_t lo = hp_bofs(h, s), hi = lo + hp_B(h, s);
+			uint32_t e = s + 1;
+			while (e < u->s1 && stv[e - u->s0] != -EINVAL && hp_bofs(h, e) == hi)
+				hi += hp_B(h, e++);
+			HIPGO(hipMemcpyAsync(h->blocks + lo, x->d + x->L.d_blk + (lo - u->blo), hi - lo,
+					     hipMemcpyDeviceToHost, st),
+			      "D2H (blocks)");
+			s = e;
+		}
+	}
+	x->u.copied = 1;
+out:
+	return rc;
+}
+
+/* Last stage: wait for the context's stream, hand the small outputs to the
+ * caller (digests / status / badmask), scatter decoded pages. */
+static int retire(const struct hp *h, struct ctxs *x)
+{
+	int rc = 0;
+	const struct sub *u = &x->u;
+	const uint32_t cnt = u->s1 - u->s0;
+	const int nsl = hp_slots(h);
+	HIPGO(hipStreamSynchronize(x->c->stream), "pipeline sync");
+	if (h->dir == HP_ENC) {
+		if (h->digests)
+			memcpy(h->digests + (uint64_t)u->s0 * nsl, x->hb + x->L.h_dig, (size_t)cnt * nsl * 8);
+	} else {
+		const int32_t *stv = (const int32_t *)(x->hb + x->L.h_status);
+		if (h->status)
+			memcpy(h->status + u->s0, stv, (size_t)cnt * 4);
+		if (h->badmask)
+			memcpy(h->badmask + u->s0, x->hb + x->L.h_bad, (size_t)cnt * 8);
+		if (hp_paged(h)) {
+			uint64_t packed = 0;
+			for (uint32_t s = u->s0; s < u->s1; s++) {
+				if (stv[s - u->s0] != -EINVAL)
+					page_copy(h, s, x->hb + x->L.h_stage + packed, 1);
+				packed += align256(hp_B(h, s));
+			}
+		}
+	}
+out:
+	x->u.live = 0;
+	return rc;
+}
+
+/* One device lane: stripes [s0, s1) of the batch on device `dev`. */
+static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
+{
+	if (s0 >= s1)
+		return 0;
+	/* scratch sized for the largest sub-batch of this lane */
+	uint64_t max_blk = 0, max_parts = 0;
+	uint32_t max_cnt = 0;
+	for (uint32_t s = s0; s < s1;) {
+		struct sub u = { .s0 = s, .s1 = sub_end(h, s, s1) };
+		sub_ranges(h, &u);
+		const uint64_t bb = dev_block_bytes(h, &u);
+		max_blk = bb > max_blk ? bb : max_blk;
+		max_parts = u.phi - u.plo > max_parts ? u.phi - u.plo : max_parts;
+		max_cnt = u.s1 - u.s0 > max_cnt ? u.s1 - u.s0 : max_cnt;
+		s = u.s1;
+	}
+	struct ctxs xs[NSTREAM];
+	memset(xs, 0, sizeof(xs));
+	int rc = 0;
+	for (int i = 0; i < NSTREAM; i++) {
+		struct ctxs *x = &xs[i];
+		layout(h, max_cnt, max_blk, max_parts, &x->L);
+		void *dv, *hv;
+		if (!(x->c = nkfs_ctx_get_on(dev))) {
+			rc = -ENOMEM;
+			goto out;
+		}
+		if ((rc = nkfs_ctx_dev(x->c, x->L.d_total, &dv)) || (rc = nkfs_ctx_host(x->c, x->L.h_total, &hv)))
+			goto out;
+		x->d = dv;
+		x->hb = hv;
+		if (h->dir == HP_DEC && hipEventCreateWithFlags(&x->u.ev, hipEventDisableTiming) != hipSuccess) {
+			x->u.ev = NULL;
+			rc = -EIO;
+			goto out;
+		}
+	}
+	/* stages per context: issue -> (decode) copy_blocks -> retire, with up
+	 * to three sub-batches in flight: sub-batch i is issued, i-1's blocks
+	 * are copied back once its status is known, i-2 retires */
+	struct ctxs *ring[NSTREAM] = {0};
+	uint32_t it = 0;
+	for (uint32_t s = s0; s < s1 && !rc; it++) {
+		struct ctxs *x = &xs[it % NSTREAM];
+		if (x->u.live && (rc = retire(h, x)))
+			break;
+		hipEvent_t ev = x->u.ev;
+		memset(&x->u, 0, sizeof(x->u));
+		x->u.ev = ev;
+		x->u.s0 = s;
+		x->u.s1 = sub_end(h, s, s1);
+		sub_ranges(h, &x->u);
+		x->u.live = 1;
+		if ((rc = issue(h, x)))
+			break;
+		ring[it % NSTREAM] = x;
+		if (h->dir == HP_DEC && it >= 1) {
+			struct ctxs *p = ring[(it - 1) % NSTREAM];
+			if (p && p->u.live && !p->u.copied && (rc = copy_blocks(h, p)))
+				break;
+		}
+		s = x->u.s1;
+	}
+	/* drain in issue order */
+	for (uint32_t j = 0; j < NSTREAM; j++) {
+		struct ctxs *x = &xs[(it + j) % NSTREAM];
+		if (!x->u.live)
+			continue;
+		int r = 0;
+		if (!rc && h->dir == HP_DEC && !x->u.copied)
+			r = copy_blocks(h, x);
+		int r2 = retire(h, x);
+		if (!rc)
+			rc = r ? r : r2;
+	}
+out:
+	for (int i = 0; i < NSTREAM; i++) {
+		if (xs[i].c) {
+			if (xs[i].u.live)
+				hipStreamSynchronize(xs[i].c->stream);
+			nkfs_ctx_put(xs[i].c);
+		}
+		if (xs[i].u.ev)
+			hipEventDestroy(xs[i].u.ev);
+	}
+	return rc;
+}
+
+static void *lane_main(void *arg)
+{
+	struct lane *l = arg;
+	l->rc = run_lane(l->h, l->dev, l->s0, l->s1);
+	return NULL;
+}
+
+/* Pin the contiguous caller buffers, cut the batch over the device lanes
+ * (byte-balanced contiguous stripe ranges) and run them. */
+static int hp_run(struct hp *h)
+{
+	if (!h->chunk)
+		h->chunk = 32ull << 20;
+	const int nsl = hp_slots(h);
+	uint64_t bend = 0, pend = 0, total = 0;
+	for (uint32_t s = 0; s < h->nstripes; s++) {
+		const uint64_t be = hp_bofs(h, s) + hp_B(h, s), pe = hp_pofs(h, s) + hp_pspan(h, s);
+		bend = be > bend ? be : bend;
+		pend = pe > pend ? pe : pend;
+		total += hp_B(h, s);
+	}
+	(void)nsl;
+	struct pin_ent *pb = NULL, *pp = NULL;
+	int rc = 0;
+	if (!hp_paged(h) && (rc = pin_take(h->blocks, bend, &pb)))
+		return rc;
+	if ((rc = pin_take(h->parts, pend, &pp))) {
+		pin_drop(pb);
+		return rc;
+	}
+	int lanes[NKFS_MAX_DEVICES];
+	int nl = nkfs_gpu_get_devices(lanes, NKFS_MAX_DEVICES);
+	if (nl > (int)h->nstripes)
+		nl = (int)h->nstripes;
+	if (nl <= 1) {
+		rc = run_lane(h, lanes[0], 0, h->nstripes);
+	} else {
+		struct lane L[NKFS_MAX_DEVICES];
+		pthread_t th[NKFS_MAX_DEVICES];
+		int started[NKFS_MAX_DEVICES] = {0};
+		uint64_t acc = 0;
+		uint32_t s = 0;
+		for (int i = 0; i < nl; i++) {
+			/* lane i ends where the running byte total passes (i+1)/nl */
+			const uint64_t goal = total * (uint64_t)(i + 1) / (uint64_t)nl;
+			uint32_t e = s;
+			while (e < h->nstripes && (i == nl - 1 || acc + hp_B(h, e) <= goal || e == s)) {
+				acc += hp_B(h, e);
+				e++;
+			}
+			L[i] = (struct lane){ h, lanes[i], s, e, 0 };
+			s = e;
+		}
+		for (int i = 1; i < nl; i++)
+			started[i] = pthread_create(&th[i], NULL, lane_main, &L[i]) == 0;
+		lane_main(&L[0]);
+		for (int i = 1; i < nl; i++) {
+			if (started[i])
+				pthread_join(th[i], NULL);
+			else
+				lane_main(&L[i]); /* no thread: run it here */
+		}
+		for (int i = 0; i < nl && !rc; i++)
+			rc = L[i].rc;
+		nkfs_use_device(nkfs_gpu_device());
+	}
+	pin_drop(pp);
+	pin_drop(pb);
+	return rc;
+}
+
+/* ----------------------------------------------------------- entry points */
+
+static int ragged_ok(const uint32_t *sizes, const uint64_t *boff, const uint64_t *poff, uint32_t nstripes,
+		     uint32_t max_block, int nsl, int k)
+{
+	for (uint32_t s = 0; s < nstripes; s++) {
+		if (!sizes[s] || sizes[s] > max_block)
+			return 0;
+		if (boff && s && boff[s] < boff[s - 1] + sizes[s - 1])
+			return 0; /* blocks overlap or go backwards */
+		if (s && poff[s] < poff[s - 1] + (uint64_t)nsl * nkfs_part_pitch(sizes[s - 1], k))
+			return 0;
+		if (poff[s] & 15)
+			return 0;
+	}
+	return 1;
+}
+
+static int pages_ok(uint8_t *const *pages, uint32_t page_size, const uint64_t *first_page, uint32_t nstripes)
+{
+	if (!pages || !first_page || page_size < 8)
+		return 0;
+	(void)nstripes;
+	return 1;
+}
 
 int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
 			 int n, int k, const uint8_t *h_ids, uint8_t *h_parts, uint64_t part_pitch,
@@ -55,92 +751,13 @@ int nkfs_nk8_encode_host(const uint8_t *h_blocks, uint64_t block_pitch, uint32_t
 	if (!h_blocks || !h_ids || !h_parts || part_pitch < nkfs_part_size(block_size, k) || (part_pitch & 15) ||
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
-	if (!chunk_bytes)
-		chunk_bytes = 32ull << 20;
-	uint32_t per = (uint32_t)(chunk_bytes / block_size);
-	if (per < 1)
-		per = 1;
-	if (per > nstripes)
-		per = nstripes;
-
-	const uint64_t bp = block_pitch ? block_pitch : block_size;
-	const uint64_t in_bytes = (uint64_t)(nstripes - 1) * bp + block_size;
-	const uint64_t parts_bytes = (uint64_t)nstripes * n * part_pitch;
-	int reg[4] = {0, 0, 0, 0}, err;
-	struct nkfs_ctx *cx[NSTREAM] = {0};
-	if ((err = pin(h_blocks, in_bytes, &reg[0])) || (err = pin(h_ids, (size_t)nstripes * n, &reg[1])) ||
-	    (err = pin(h_parts, parts_bytes, &reg[2])) ||
-	    (err = pin(h_digests, h_digests ? (size_t)nstripes * n * 8 : 0, &reg[3])))
-		goto unpin;
-
-	/* per context: blocks | parts | ids | digests (device) */
-	const uint64_t dblk = (uint64_t)per * bp;
-	const uint64_t dparts = (uint64_t)per * n * part_pitch;
-	const uint64_t dids = ((uint64_t)per * n + 255) & ~255ull;
-	const uint64_t ddig = (uint64_t)per * n * 8;
-	const uint64_t slot = ((dblk + 255) & ~255ull) + dparts + dids + ddig;
-	void *dev[NSTREAM];
-	hipError_t e = hipSuccess;
-	for (int i = 0; i < NSTREAM; i++) {
-		cx[i] = nkfs_ctx_get();
-		if (!cx[i]) {
-			err = -ENOMEM;
-			goto out;
-		}
-		if ((err = nkfs_ctx_dev(cx[i], slot, &dev[i])))
-			goto out;
-	}
-	for (uint32_t s0 = 0, it = 0; s0 < nstripes; s0 += per, it++) {
-		const uint32_t cnt = nstripes - s0 < per ? nstripes - s0 : per;
-		hipStream_t s = cx[it % NSTREAM]->stream;
-		uint8_t *d = (uint8_t *)dev[it % NSTREAM];
-		uint8_t *d_blk = d, *d_parts = d + ((dblk + 255) & ~255ull);
-		uint8_t *d_ids = d_parts + dparts;
-		uint64_t *d_dig = (uint64_t *)(d_ids + dids);
-		const uint64_t nin = (uint64_t)(cnt - 1) * bp + block_size;
-		if ((e = hipMemcpyAsync(d_blk, h_blocks + (uint64_t)s0 * bp, nin, hipMemcpyHostToDevice, s)) ||
-		    (e = hipMemcpyAsync(d_ids, h_ids + (uint64_t)s0 * n, (size_t)cnt * n, hipMemcpyHostToDevice, s))) {
-			err = nkfs_hip_fail("H2D", (int)e);
-			goto out;
-		}
-		struct nkfs_geom g = { d_blk, bp, block_size, NULL, NULL, d_parts, part_pitch, NULL, cnt, n, k, NULL, 0, 0 };
-		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), s)))
-			goto out;
-		if ((e = hipMemcpyAsync(h_parts + (uint64_t)s0 * n * part_pitch, d_parts, (uint64_t)cnt * n * part_pitch,
-					hipMemcpyDeviceToHost, s)) ||
-		    (h_digests && (e = hipMemcpyAsync(h_digests + (uint64_t)s0 * n, d_dig, (size_t)cnt * n * 8,
-						       hipMemcpyDeviceToHost, s)))) {
-			err = nkfs_hip_fail("D2H", (int)e);
-			goto out;
-		}
-	}
-	err = 0;
-out:
-	for (int i = 0; i < NSTREAM; i++)
-		if (cx[i]) {
-			if ((e = hipStreamSynchronize(cx[i]->stream)) != hipSuccess && !err)
-				err = nkfs_hip_fail("pipeline sync", (int)e);
-			nkfs_ctx_put(cx[i]);
-		}
-unpin:
-	if (reg[0])
-		hipHostUnregister((void *)h_blocks);
-	if (reg[1])
-		hipHostUnregister((void *)h_ids);
-	if (reg[2])
-		hipHostUnregister(h_parts);
-	if (reg[3])
-		hipHostUnregister(h_digests);
-	return err;
+	struct hp h = { .dir = HP_ENC, .n = n, .k = k, .nstripes = nstripes, .max_block = block_size,
+			.block_size = block_size, .block_pitch = nstripes > 1 ? block_pitch : block_size,
+			.part_pitch = part_pitch, .blocks = (uint8_t *)h_blocks, .parts = h_parts, .ids = h_ids,
+			.digests = h_digests, .chunk = chunk_bytes };
+	return hp_run(&h);
 }
 
-/* Ragged host batch: stripe s is h_block_size[s] bytes at h_blocks +
- * h_block_off[s]; its n parts go to h_parts + h_part_off[s] + i*pitch(B_s).
- * Offsets must be non-decreasing in s (a packed layout), so a run of
- * consecutive stripes is one contiguous byte range on both sides: each
- * sub-batch is one H2D of its blocks, one launch of the ragged encode and one
- * D2H of its parts.  The device geometry points its bases at (device buffer -
- * first offset), so the caller's offsets are copied unchanged. */
 int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks, const uint64_t *h_block_off, const uint32_t *h_block_size,
 				uint32_t max_block_size, uint32_t nstripes, int n, int k, const uint8_t *h_ids,
 				uint8_t *h_parts, const uint64_t *h_part_off, uint64_t *h_digests, uint64_t chunk_bytes)
@@ -151,137 +768,107 @@ int nkfs_nk8_encode_ragged_host(const uint8_t *h_blocks, const uint64_t *h_block
 		return -EAGAIN;
 	if (!nstripes)
 		return 0;
-	if (!h_blocks || !h_block_off || !h_block_size || !h_ids || !h_parts || !h_part_off)
+	if (!h_blocks || !h_block_off || !h_block_size || !h_ids || !h_parts || !h_part_off ||
+	    !ragged_ok(h_block_size, h_block_off, h_part_off, nstripes, max_block_size, n, k))
 		return -EINVAL;
-	if (!chunk_bytes)
-		chunk_bytes = 32ull << 20;
+	struct hp h = { .dir = HP_ENC, .n = n, .k = k, .nstripes = nstripes, .max_block = max_block_size,
+			.sizes = h_block_size, .boff = h_block_off, .poff = h_part_off, .blocks = (uint8_t *)h_blocks,
+			.parts = h_parts, .ids = h_ids, .digests = h_digests, .chunk = chunk_bytes };
+	return hp_run(&h);
+}
 
-	/* sub-batches: [first stripe, end) with <= chunk_bytes of blocks (>= 1
-	 * stripe); byte extents of every range on both sides */
-	uint64_t in_end = 0, parts_end = 0, max_in = 0, max_parts = 0, max_cnt = 0;
-	for (uint32_t s = 0; s < nstripes; s++) {
-		if (h_block_size[s] > max_block_size || (s && (h_block_off[s] < h_block_off[s - 1] ||
-							     h_part_off[s] < h_part_off[s - 1])))
-			return -EINVAL;
-		const uint64_t e1 = h_block_off[s] + h_block_size[s];
-		const uint64_t e2 = h_part_off[s] + (uint64_t)n * nkfs_part_pitch(h_block_size[s], k);
-		in_end = e1 > in_end ? e1 : in_end;
-		parts_end = e2 > parts_end ? e2 : parts_end;
-	}
-	for (uint32_t s0 = 0; s0 < nstripes;) {
-		uint32_t s1 = s0 + 1;
-		uint64_t hi = h_block_off[s0] + h_block_size[s0];
-		while (s1 < nstripes && h_block_off[s1] + h_block_size[s1] - h_block_off[s0] <= chunk_bytes) {
-			const uint64_t e = h_block_off[s1] + h_block_size[s1];
-			hi = e > hi ? e : hi;
-			s1++;
-		}
-		uint64_t phi = 0;
-		for (uint32_t s = s0; s < s1; s++) {
-			const uint64_t e = h_part_off[s] + (uint64_t)n * nkfs_part_pitch(h_block_size[s], k);
-			phi = e > phi ? e : phi;
-		}
-		if (hi - h_block_off[s0] > max_in)
-			max_in = hi - h_block_off[s0];
-		if (phi - h_part_off[s0] > max_parts)
-			max_parts = phi - h_part_off[s0];
-		if (s1 - s0 > max_cnt)
-			max_cnt = s1 - s0;
-		s0 = s1;
-	}
+int nkfs_nk8_encode_pages(const uint8_t *const *h_pages, uint32_t page_size, const uint64_t *h_first_page,
+			  const uint32_t *h_block_size, uint32_t max_block_size, uint32_t nstripes, int n, int k,
+			  const uint8_t *h_ids, uint8_t *h_parts, const uint64_t *h_part_off, uint64_t *h_digests,
+			  uint64_t chunk_bytes)
+{
+	if (nkfs_bad_params(max_block_size, n, k))
+		return -EINVAL;
+	if (!nkfs_gpu_ready())
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!h_block_size || !h_ids || !h_parts || !h_part_off ||
+	    !pages_ok((uint8_t *const *)h_pages, page_size, h_first_page, nstripes) ||
+	    !ragged_ok(h_block_size, NULL, h_part_off, nstripes, max_block_size, n, k))
+		return -EINVAL;
+	struct hp h = { .dir = HP_ENC, .n = n, .k = k, .nstripes = nstripes, .max_block = max_block_size,
+			.sizes = h_block_size, .poff = h_part_off, .pages = (uint8_t *const *)h_pages,
+			.first_page = h_first_page, .page_size = page_size, .parts = h_parts, .ids = h_ids,
+			.digests = h_digests, .chunk = chunk_bytes };
+	return hp_run(&h);
+}
 
-	int reg[7] = {0, 0, 0, 0, 0, 0, 0}, err;
-	struct nkfs_ctx *cx[NSTREAM] = {0};
-	if ((err = pin(h_blocks, in_end, &reg[0])) || (err = pin(h_ids, (size_t)nstripes * n, &reg[1])) ||
-	    (err = pin(h_parts, parts_end, &reg[2])) ||
-	    (err = pin(h_digests, h_digests ? (size_t)nstripes * n * 8 : 0, &reg[3])) ||
-	    (err = pin(h_block_off, (size_t)nstripes * 8, &reg[4])) ||
-	    (err = pin(h_block_size, (size_t)nstripes * 4, &reg[5])) ||
-	    (err = pin(h_part_off, (size_t)nstripes * 8, &reg[6])))
-		goto unpin;
+static int dec_args_ok(int n_slots, int navail, int k, uint32_t block_size, const uint8_t *ids, const uint8_t *avail)
+{
+	return !nkfs_bad_params(block_size, navail, k) && n_slots >= 1 && n_slots <= 255 && ids && avail;
+}
 
-	/* per context: blocks | parts | block_off | part_off | sizes | ids | digests */
-	const uint64_t a_in = (max_in + 255) & ~255ull, a_parts = (max_parts + 255) & ~255ull;
-	const uint64_t a_off = (max_cnt * 8 + 255) & ~255ull, a_sz = (max_cnt * 4 + 255) & ~255ull;
-	const uint64_t a_ids = (max_cnt * n + 255) & ~255ull, a_dig = max_cnt * n * 8;
-	const uint64_t slot = a_in + a_parts + 2 * a_off + a_sz + a_ids + a_dig;
-	void *dev[NSTREAM];
-	hipError_t e = hipSuccess;
-	for (int i = 0; i < NSTREAM; i++) {
-		cx[i] = nkfs_ctx_get();
-		if (!cx[i]) {
-			err = -ENOMEM;
-			goto out;
-		}
-		if ((err = nkfs_ctx_dev(cx[i], slot, &dev[i])))
-			goto out;
-	}
-	for (uint32_t s0 = 0, it = 0; s0 < nstripes; it++) {
-		uint32_t s1 = s0 + 1;
-		uint64_t hi = h_block_off[s0] + h_block_size[s0];
-		while (s1 < nstripes && h_block_off[s1] + h_block_size[s1] - h_block_off[s0] <= chunk_bytes) {
-			const uint64_t e1 = h_block_off[s1] + h_block_size[s1];
-			hi = e1 > hi ? e1 : hi;
-			s1++;
-		}
-		uint64_t phi = 0;
-		for (uint32_t s = s0; s < s1; s++) {
-			const uint64_t e2 = h_part_off[s] + (uint64_t)n * nkfs_part_pitch(h_block_size[s], k);
-			phi = e2 > phi ? e2 : phi;
-		}
-		const uint32_t cnt = s1 - s0;
-		const uint64_t lo = h_block_off[s0], plo = h_part_off[s0];
-		hipStream_t st = cx[it % NSTREAM]->stream;
-		uint8_t *d = (uint8_t *)dev[it % NSTREAM];
-		uint8_t *d_blk = d, *d_parts = d + a_in;
-		uint64_t *d_boff = (uint64_t *)(d_parts + a_parts), *d_poff = (uint64_t *)((uint8_t *)d_boff + a_off);
-		uint32_t *d_sz = (uint32_t *)((uint8_t *)d_poff + a_off);
-		uint8_t *d_ids = (uint8_t *)d_sz + a_sz;
-		uint64_t *d_dig = (uint64_t *)(d_ids + a_ids);
-		if ((e = hipMemcpyAsync(d_blk, h_blocks + lo, hi - lo, hipMemcpyHostToDevice, st)) ||
-		    (e = hipMemcpyAsync(d_boff, h_block_off + s0, (size_t)cnt * 8, hipMemcpyHostToDevice, st)) ||
-		    (e = hipMemcpyAsync(d_poff, h_part_off + s0, (size_t)cnt * 8, hipMemcpyHostToDevice, st)) ||
-		    (e = hipMemcpyAsync(d_sz, h_block_size + s0, (size_t)cnt * 4, hipMemcpyHostToDevice, st)) ||
-		    (e = hipMemcpyAsync(d_ids, h_ids + (uint64_t)s0 * n, (size_t)cnt * n, hipMemcpyHostToDevice, st))) {
-			err = nkfs_hip_fail("H2D", (int)e);
-			goto out;
-		}
-		/* bases shifted by the range's first offsets: base + off[s] lands
-		 * inside this context's buffers */
-		struct nkfs_geom g = { d_blk - lo, 0, max_block_size, d_boff, d_sz, d_parts - plo, 0, d_poff, cnt, n, k,
-				       NULL, 0, 0 };
-		if ((err = nkfs_launch_encode(&g, d_ids, h_digests ? d_dig : NULL, nkfs_gf(), st)))
-			goto out;
-		if ((e = hipMemcpyAsync(h_parts + plo, d_parts, phi - plo, hipMemcpyDeviceToHost, st)) ||
-		    (h_digests && (e = hipMemcpyAsync(h_digests + (uint64_t)s0 * n, d_dig, (size_t)cnt * n * 8,
-						       hipMemcpyDeviceToHost, st)))) {
-			err = nkfs_hip_fail("D2H", (int)e);
-			goto out;
-		}
-		s0 = s1;
-	}
-	err = 0;
-out:
-	for (int i = 0; i < NSTREAM; i++)
-		if (cx[i]) {
-			if ((e = hipStreamSynchronize(cx[i]->stream)) != hipSuccess && !err)
-				err = nkfs_hip_fail("pipeline sync", (int)e);
-			nkfs_ctx_put(cx[i]);
-		}
-unpin:
-	if (reg[0])
-		hipHostUnregister((void *)h_blocks);
-	if (reg[1])
-		hipHostUnregister((void *)h_ids);
-	if (reg[2])
-		hipHostUnregister(h_parts);
-	if (reg[3])
-		hipHostUnregister(h_digests);
-	if (reg[4])
-		hipHostUnregister((void *)h_block_off);
-	if (reg[5])
-		hipHostUnregister((void *)h_block_size);
-	if (reg[6])
-		hipHostUnregister((void *)h_part_off);
-	return err;
+int nkfs_nk8_decode_host(const uint8_t *h_parts, uint64_t part_pitch, int n_slots, const uint8_t *h_ids,
+			 const uint8_t *h_avail, int navail, int k, uint32_t block_size, uint8_t *h_blocks,
+			 uint64_t block_pitch, uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect,
+			 uint64_t *h_badmask, uint64_t chunk_bytes)
+{
+	if (!dec_args_ok(n_slots, navail, k, block_size, h_ids, h_avail))
+		return -EINVAL;
+	if (!nkfs_gpu_ready())
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!h_parts || !h_blocks || part_pitch < nkfs_part_size(block_size, k) || (part_pitch & 15) ||
+	    (nstripes > 1 && block_pitch < block_size))
+		return -EINVAL;
+	struct hp h = { .dir = HP_DEC, .n = n_slots, .k = k, .n_slots = n_slots, .navail = navail,
+			.nstripes = nstripes, .max_block = block_size, .block_size = block_size,
+			.block_pitch = nstripes > 1 ? block_pitch : block_size, .part_pitch = part_pitch,
+			.blocks = h_blocks, .parts = (uint8_t *)h_parts, .ids = h_ids, .avail = h_avail,
+			.expect = h_expect, .badmask = h_expect ? h_badmask : NULL, .status = h_status,
+			.chunk = chunk_bytes };
+	return hp_run(&h);
+}
+
+int nkfs_nk8_decode_ragged_host(const uint8_t *h_parts, const uint64_t *h_part_off, int n_slots,
+				const uint8_t *h_ids, const uint8_t *h_avail, int navail, int k, uint8_t *h_blocks,
+				const uint64_t *h_block_off, const uint32_t *h_block_size, uint32_t max_block_size,
+				uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect, uint64_t *h_badmask,
+				uint64_t chunk_bytes)
+{
+	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail))
+		return -EINVAL;
+	if (!nkfs_gpu_ready())
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!h_parts || !h_part_off || !h_blocks || !h_block_off || !h_block_size ||
+	    !ragged_ok(h_block_size, h_block_off, h_part_off, nstripes, max_block_size, n_slots, k))
+		return -EINVAL;
+	struct hp h = { .dir = HP_DEC, .n = n_slots, .k = k, .n_slots = n_slots, .navail = navail,
+			.nstripes = nstripes, .max_block = max_block_size, .sizes = h_block_size,
+			.boff = h_block_off, .poff = h_part_off, .blocks = h_blocks, .parts = (uint8_t *)h_parts,
+			.ids = h_ids, .avail = h_avail, .expect = h_expect, .badmask = h_expect ? h_badmask : NULL,
+			.status = h_status, .chunk = chunk_bytes };
+	return hp_run(&h);
+}
+
+int nkfs_nk8_decode_pages(const uint8_t *h_parts, const uint64_t *h_part_off, int n_slots, const uint8_t *h_ids,
+			  const uint8_t *h_avail, int navail, int k, uint8_t *const *h_pages, uint32_t page_size,
+			  const uint64_t *h_first_page, const uint32_t *h_block_size, uint32_t max_block_size,
+			  uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect, uint64_t *h_badmask,
+			  uint64_t chunk_bytes)
+{
+	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail))
+		return -EINVAL;
+	if (!nkfs_gpu_ready())
+		return -EAGAIN;
+	if (!nstripes)
+		return 0;
+	if (!h_parts || !h_part_off || !h_block_size || !pages_ok(h_pages, page_size, h_first_page, nstripes) ||
+	    !ragged_ok(h_block_size, NULL, h_part_off, nstripes, max_block_size, n_slots, k))
+		return -EINVAL;
+	struct hp h = { .dir = HP_DEC, .n = n_slots, .k = k, .n_slots = n_slots, .navail = navail,
+			.nstripes = nstripes, .max_block = max_block_size, .sizes = h_block_size,
+			.poff = h_part_off, .pages = h_pages, .first_page = h_first_page, .page_size = page_size,
+			.parts = (uint8_t *)h_parts, .ids = h_ids, .avail = h_avail, .expect = h_expect,
+			.badmask = h_expect ? h_badmask : NULL, .status = h_status, .chunk = chunk_bytes };
+	return hp_run(&h);
 }

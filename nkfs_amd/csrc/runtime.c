@@ -3,11 +3,13 @@
  * include/nkfs_gpu.h.  Host C over the HIP runtime; every computation is a
  * kernel launched through nkfs_internal.h.
  *
- * State: one GPU (chosen at init), one device copy of the GF(2^8)
- * log/antilog tables, and a pool of per-call contexts (stream + growable
- * device/pinned scratch) so that the compatibility entry points are
- * reentrant and thread-safe after init like the reference's
- * (SURVEY.md §8(b) "Threading").
+ * State: the library's device (chosen at init: the compatibility entry
+ * points run there), and per device a copy of the GF(2^8) log/antilog
+ * tables plus a pool of per-call contexts (stream + growable device/pinned
+ * scratch), so that every entry point is reentrant and thread-safe after
+ * init like the reference's (SURVEY.md §8(b) "Threading").  Batched device
+ * calls run on the device of the caller's stream; the host-memory entry
+ * points spread a batch over the device lanes of nkfs_gpu_set_devices.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -23,10 +25,23 @@
 
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 static int g_ready;
-static int g_device = -1;
+static int g_device = -1; /* the library's device: compatibility entry points run here */
 static int g_cus = 256;
-static void *g_gf;
-static struct nkfs_ctx *g_pool;
+
+/* Per-device state: GF tables and an idle pool of per-call contexts.  A
+ * device is set up on first use (nkfs_gpu_init for the library's device,
+ * nkfs_gpu_set_devices or a batched call on another device's stream). */
+struct nkfs_dev {
+	int ready;
+	void *gf;
+	struct nkfs_ctx *pool;
+};
+static struct nkfs_dev g_dev[NKFS_MAX_DEVICES];
+
+/* Devices the host-memory entry points spread a batch over (one lane per
+ * entry, repeats allowed); empty = the library's device. */
+static int g_lanes[NKFS_MAX_DEVICES];
+static int g_nlanes;
 
 /* Measured defaults; nkfs_tune_set replaces them. */
 struct nkfs_tune nkfs_g_tune = {
@@ -38,6 +53,7 @@ struct nkfs_tune nkfs_g_tune = {
 	.enc_nib = -1,
 	.enc_units = 0,
 	.size_order = 1,
+	.enc_prefetch = 1,
 };
 
 void nkfs_tune_get(struct nkfs_tune *t)
@@ -53,7 +69,7 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||
-	    (t->size_order != 0 && t->size_order != 1))
+	    (t->size_order != 0 && t->size_order != 1) || t->enc_prefetch < 1 || t->enc_prefetch > 2)
 		return -EINVAL;
 	nkfs_g_tune = *t;
 	return 0;
@@ -72,14 +88,54 @@ int nkfs_hip_fail(const char *what, int err)
 			return nkfs_hip_fail(#call, (int)e_);        \
 	} while (0)
 
+/* make `dev` the calling thread's current device (no call when it already is) */
+int nkfs_use_device(int dev)
+{
+	int cur = -1;
+	if (hipGetDevice(&cur) == hipSuccess && cur == dev)
+		return 0;
+	return hipSetDevice(dev) == hipSuccess ? 0 : -EIO;
+}
+
+/* GF tables on `dev`, under g_lock.  Leaves `dev` current. */
+static int dev_setup_locked(int dev)
+{
+	struct nkfs_dev *d = &g_dev[dev];
+	if (d->ready)
+		return nkfs_use_device(dev);
+	hipError_t e = hipSetDevice(dev);
+	if (e == hipSuccess)
+		e = hipMalloc(&d->gf, nkfs_gf_tables_bytes());
+	if (e != hipSuccess)
+		return nkfs_hip_fail("device setup", (int)e);
+	int rc = nkfs_launch_gf_init(d->gf, NULL);
+	if (!rc && (e = hipDeviceSynchronize()) != hipSuccess)
+		rc = nkfs_hip_fail("gf table build", (int)e);
+	if (rc) {
+		hipFree(d->gf);
+		d->gf = NULL;
+		return rc;
+	}
+	d->ready = 1;
+	return 0;
+}
+
+static int device_count(void)
+{
+	int count = 0;
+	if (hipGetDeviceCount(&count) != hipSuccess)
+		return 0;
+	return count < NKFS_MAX_DEVICES ? count : NKFS_MAX_DEVICES;
+}
+
 int nkfs_gpu_init(int device)
 {
 	int rc = 0;
 	pthread_mutex_lock(&g_lock);
 	if (g_ready)
 		goto out;
-	int count = 0;
-	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+	int count = device_count();
+	if (count <= 0) {
 		fprintf(stderr, "nkfs: no HIP device visible; the MI355X path has no CPU fallback\n");
 		rc = -ENODEV;
 		goto out;
@@ -91,25 +147,12 @@ int nkfs_gpu_init(int device)
 		else if (hipGetDevice(&device) != hipSuccess)
 			device = 0;
 	}
-	if (device >= count) {
+	if (device < 0 || device >= count) {
 		rc = -ENODEV;
 		goto out;
 	}
-	hipError_t e = hipSetDevice(device);
-	if (e == hipSuccess)
-		e = hipMalloc(&g_gf, nkfs_gf_tables_bytes());
-	if (e != hipSuccess) {
-		rc = nkfs_hip_fail("device setup", (int)e);
+	if ((rc = dev_setup_locked(device)))
 		goto out;
-	}
-	rc = nkfs_launch_gf_init(g_gf, NULL);
-	if (!rc && (e = hipDeviceSynchronize()) != hipSuccess)
-		rc = nkfs_hip_fail("gf table build", (int)e);
-	if (rc) {
-		hipFree(g_gf);
-		g_gf = NULL;
-		goto out;
-	}
 	int cus = 0;
 	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
 		g_cus = cus;
@@ -122,9 +165,81 @@ out:
 
 int nkfs_gpu_ready(void) { return g_ready; }
 
+int nkfs_gpu_device(void) { return g_ready ? g_device : -1; }
+
+int nkfs_gpu_count(void) { return device_count(); }
+
 int nkfs_cu_count(void) { return g_cus; }
 
-const void *nkfs_gf(void) { return g_gf; }
+/* GF tables of `dev`, set up on first use; NULL when it cannot be. */
+const void *nkfs_gf_on(int dev)
+{
+	if (dev < 0 || dev >= NKFS_MAX_DEVICES)
+		return NULL;
+	if (g_dev[dev].ready)
+		return g_dev[dev].gf;
+	pthread_mutex_lock(&g_lock);
+	int cur = -1;
+	(void)hipGetDevice(&cur);
+	int rc = dev < device_count() ? dev_setup_locked(dev) : -ENODEV;
+	if (cur >= 0)
+		nkfs_use_device(cur);
+	pthread_mutex_unlock(&g_lock);
+	return rc ? NULL : g_dev[dev].gf;
+}
+
+/* GF tables of the device a launch on `stream` runs on (NULL stream: the
+ * calling thread's current device). */
+const void *nkfs_gf_for(void *stream)
+{
+	int dev = -1;
+	if (stream) {
+		if (hipStreamGetDevice((hipStream_t)stream, &dev) != hipSuccess)
+			return NULL;
+	} else if (hipGetDevice(&dev) != hipSuccess) {
+		return NULL;
+	}
+	return nkfs_gf_on(dev);
+}
+
+const void *nkfs_gf(void) { return g_ready ? g_dev[g_device].gf : NULL; }
+
+int nkfs_gpu_set_devices(const int *devices, int count)
+{
+	if (count < 0 || count > NKFS_MAX_DEVICES || (count && !devices))
+		return -EINVAL;
+	if (!g_ready)
+		return -EAGAIN;
+	const int ndev = device_count();
+	for (int i = 0; i < count; i++)
+		if (devices[i] < 0 || devices[i] >= ndev)
+			return -ENODEV;
+	int rc = 0;
+	pthread_mutex_lock(&g_lock);
+	int cur = -1;
+	(void)hipGetDevice(&cur);
+	for (int i = 0; i < count && !rc; i++)
+		rc = dev_setup_locked(devices[i]);
+	if (!rc) {
+		for (int i = 0; i < count; i++)
+			g_lanes[i] = devices[i];
+		g_nlanes = count;
+	}
+	if (cur >= 0)
+		nkfs_use_device(cur);
+	pthread_mutex_unlock(&g_lock);
+	return rc;
+}
+
+int nkfs_gpu_get_devices(int *devices, int max)
+{
+	pthread_mutex_lock(&g_lock);
+	int n = g_nlanes ? g_nlanes : (g_ready ? 1 : 0);
+	for (int i = 0; i < n && i < max && devices; i++)
+		devices[i] = g_nlanes ? g_lanes[i] : g_device;
+	pthread_mutex_unlock(&g_lock);
+	return n;
+}
 
 static void ctx_destroy(struct nkfs_ctx *c)
 {
@@ -135,71 +250,102 @@ static void ctx_destroy(struct nkfs_ctx *c)
 	free(c);
 }
 
-void nkfs_gpu_release(void)
+static void pools_drain(struct nkfs_ctx **taken)
 {
-	pthread_mutex_lock(&g_lock);
-	if (g_ready) {
-		hipSetDevice(g_device);
-		while (g_pool) {
-			struct nkfs_ctx *c = g_pool;
-			g_pool = c->next;
+	for (int d = 0; d < NKFS_MAX_DEVICES; d++) {
+		struct nkfs_ctx *pool = taken[d];
+		if (!pool)
+			continue;
+		hipSetDevice(d);
+		while (pool) {
+			struct nkfs_ctx *c = pool;
+			pool = c->next;
 			ctx_destroy(c);
 		}
-		hipFree(g_gf);
-		g_gf = NULL;
-		g_ready = 0;
 	}
+}
+
+void nkfs_gpu_release(void)
+{
+	struct nkfs_ctx *taken[NKFS_MAX_DEVICES] = {0};
+	pthread_mutex_lock(&g_lock);
+	for (int d = 0; d < NKFS_MAX_DEVICES; d++) {
+		taken[d] = g_dev[d].pool;
+		g_dev[d].pool = NULL;
+	}
+	pools_drain(taken);
+	for (int d = 0; d < NKFS_MAX_DEVICES; d++)
+		if (g_dev[d].ready) {
+			hipSetDevice(d);
+			hipFree(g_dev[d].gf);
+			g_dev[d].gf = NULL;
+			g_dev[d].ready = 0;
+		}
+	g_ready = 0;
+	g_nlanes = 0;
 	pthread_mutex_unlock(&g_lock);
 }
 
 void nkfs_ctx_trim(void)
 {
+	struct nkfs_ctx *taken[NKFS_MAX_DEVICES] = {0};
 	pthread_mutex_lock(&g_lock);
-	struct nkfs_ctx *pool = g_pool;
-	g_pool = NULL;
-	pthread_mutex_unlock(&g_lock);
-	if (pool)
-		hipSetDevice(g_device);
-	while (pool) {
-		struct nkfs_ctx *c = pool;
-		pool = c->next;
-		ctx_destroy(c);
+	for (int d = 0; d < NKFS_MAX_DEVICES; d++) {
+		taken[d] = g_dev[d].pool;
+		g_dev[d].pool = NULL;
 	}
+	pthread_mutex_unlock(&g_lock);
+	pools_drain(taken);
+	if (g_ready)
+		nkfs_use_device(g_device);
 }
 
-struct nkfs_ctx *nkfs_ctx_get(void)
+/* A per-call context (stream + scratch) on `dev`, from its idle pool or new;
+ * leaves `dev` current for the calling thread. */
+struct nkfs_ctx *nkfs_ctx_get_on(int dev)
 {
 	struct nkfs_ctx *c = NULL;
-	if (!g_ready)
+	if (!g_ready || dev < 0 || dev >= NKFS_MAX_DEVICES || !nkfs_gf_on(dev))
 		return NULL;
 	pthread_mutex_lock(&g_lock);
-	if (g_pool) {
-		c = g_pool;
-		g_pool = c->next;
+	if (g_dev[dev].pool) {
+		c = g_dev[dev].pool;
+		g_dev[dev].pool = c->next;
 	}
 	pthread_mutex_unlock(&g_lock);
-	if (hipSetDevice(g_device) != hipSuccess)
+	if (nkfs_use_device(dev))
 		goto fail;
 	if (!c) {
 		c = calloc(1, sizeof(*c));
 		if (!c)
 			return NULL;
+		c->dev = dev;
 		if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 			goto fail;
 	}
 	return c;
 fail:
-	free(c);
+	if (c)
+		nkfs_ctx_put(c);
 	return NULL;
+}
+
+struct nkfs_ctx *nkfs_ctx_get(void)
+{
+	return g_ready ? nkfs_ctx_get_on(g_device) : NULL;
 }
 
 void nkfs_ctx_put(struct nkfs_ctx *c)
 {
 	if (!c)
 		return;
+	if (!c->stream) {
+		free(c);
+		return;
+	}
 	pthread_mutex_lock(&g_lock);
-	c->next = g_pool;
-	g_pool = c;
+	c->next = g_dev[c->dev].pool;
+	g_dev[c->dev].pool = c;
 	pthread_mutex_unlock(&g_lock);
 }
 
@@ -266,9 +412,12 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 	if (!d_blocks || !d_ids || !d_parts || part_pitch < nkfs_part_size(block_size, k) || (part_pitch & 15) ||
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
+	const void *gf = nkfs_gf_for(stream);
+	if (!gf)
+		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
 			       nstripes, n, k, NULL, 0, 0 };
-	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
+	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
 int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off, const uint32_t *d_block_size,
@@ -283,9 +432,12 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 		return 0;
 	if (!d_blocks || !d_block_off || !d_block_size || !d_ids || !d_parts || !d_part_off)
 		return -EINVAL;
+	const void *gf = nkfs_gf_for(stream);
+	if (!gf)
+		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
 			       nstripes, n, k, NULL, 0, 0 };
-	return nkfs_launch_encode(&g, d_ids, d_digests, g_gf, stream);
+	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
 uint64_t nkfs_decode_workspace(uint32_t nstripes, int k)
@@ -307,9 +459,12 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 	if (!d_parts || !d_ids || !d_avail || !d_blocks || !d_work || part_pitch < nkfs_part_size(block_size, k) ||
 	    (nstripes > 1 && block_pitch < block_size))
 		return -EINVAL;
+	const void *gf = nkfs_gf_for(stream);
+	if (!gf)
+		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
 			       nstripes, n_slots, k, NULL, 0, 0 };
-	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, d_expect,
+	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
 				  d_badmask);
 }
 
@@ -321,10 +476,11 @@ int nkfs_nk8_decode(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, co
 			     block_pitch, nstripes, d_work, d_status, NULL, NULL, stream);
 }
 
-int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots, const uint8_t *d_ids,
-			   const uint8_t *d_avail, int navail, int k, uint8_t *d_blocks, const uint64_t *d_block_off,
-			   const uint32_t *d_block_size, uint32_t max_block_size, uint32_t nstripes, void *d_work,
-			   int32_t *d_status, void *stream)
+static int decode_ragged_common(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots,
+				const uint8_t *d_ids, const uint8_t *d_avail, int navail, int k, uint8_t *d_blocks,
+				const uint64_t *d_block_off, const uint32_t *d_block_size, uint32_t max_block_size,
+				uint32_t nstripes, void *d_work, int32_t *d_status, const uint64_t *d_expect,
+				uint64_t *d_badmask, void *stream)
 {
 	if (nkfs_bad_params(max_block_size, navail, k) || n_slots < 1 || n_slots > 255)
 		return -EINVAL;
@@ -334,9 +490,35 @@ int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off, i
 		return 0;
 	if (!d_parts || !d_part_off || !d_ids || !d_avail || !d_blocks || !d_block_off || !d_block_size || !d_work)
 		return -EINVAL;
+	const void *gf = nkfs_gf_for(stream);
+	if (!gf)
+		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, (uint8_t *)d_parts, 0,
 			       d_part_off, nstripes, n_slots, k, NULL, 0, 0 };
-	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, g_gf, stream, NULL, NULL);
+	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
+				  d_badmask);
+}
+
+int nkfs_nk8_decode_ragged(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots, const uint8_t *d_ids,
+			   const uint8_t *d_avail, int navail, int k, uint8_t *d_blocks, const uint64_t *d_block_off,
+			   const uint32_t *d_block_size, uint32_t max_block_size, uint32_t nstripes, void *d_work,
+			   int32_t *d_status, void *stream)
+{
+	return decode_ragged_common(d_parts, d_part_off, n_slots, d_ids, d_avail, navail, k, d_blocks, d_block_off,
+				    d_block_size, max_block_size, nstripes, d_work, d_status, NULL, NULL, stream);
+}
+
+int nkfs_nk8_decode_ragged_verify(const uint8_t *d_parts, const uint64_t *d_part_off, int n_slots,
+				  const uint8_t *d_ids, const uint8_t *d_avail, int navail, int k, uint8_t *d_blocks,
+				  const uint64_t *d_block_off, const uint32_t *d_block_size, uint32_t max_block_size,
+				  uint32_t nstripes, void *d_work, int32_t *d_status, const uint64_t *d_expect,
+				  uint64_t *d_badmask, void *stream)
+{
+	if (!d_expect)
+		return -EINVAL;
+	return decode_ragged_common(d_parts, d_part_off, n_slots, d_ids, d_avail, navail, k, d_blocks, d_block_off,
+				    d_block_size, max_block_size, nstripes, d_work, d_status, d_expect, d_badmask,
+				    stream);
 }
 
 int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch, int n_slots, const uint8_t *d_ids,
@@ -406,7 +588,7 @@ int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_si
 void *nkfs_dev_alloc(size_t bytes)
 {
 	void *p = NULL;
-	if (!g_ready || hipSetDevice(g_device) != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess)
+	if (!g_ready || nkfs_use_device(g_device) || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess)
 		return NULL;
 	return p;
 }

@@ -7,7 +7,10 @@
 
 #include <hip/hip_runtime_api.h>
 
+#define NKFS_MAX_DEVICES 16
+
 struct nkfs_ctx {
+	int dev;      /* device the stream and scratch belong to */
 	hipStream_t stream;
 	void *dbuf;   /* device scratch */
 	size_t dcap;
@@ -16,11 +19,15 @@ struct nkfs_ctx {
 	struct nkfs_ctx *next;
 };
 
-struct nkfs_ctx *nkfs_ctx_get(void);
+struct nkfs_ctx *nkfs_ctx_get(void);          /* on the library's device */
+struct nkfs_ctx *nkfs_ctx_get_on(int dev);
 void nkfs_ctx_put(struct nkfs_ctx *c);
 int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out);
-const void *nkfs_gf(void);
+const void *nkfs_gf(void);                   /* tables on the library's device */
+const void *nkfs_gf_on(int dev);
+const void *nkfs_gf_for(void *stream);       /* tables on the device of `stream` */
+int nkfs_use_device(int dev);
 void nkfs_gpu_release(void);
 void nkfs_ctx_trim(void);
 int nkfs_bad_params(uint32_t block_size, int n, int k);

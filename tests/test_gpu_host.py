@@ -1,0 +1,396 @@
+"""Host-memory entry points (include/nkfs_gpu.h, pipeline.c) through the
+C-ABI: PUT/GET from contiguous host buffers and from page lists
+(core/upages.c:91-148, core/net.c:145-265), several sub-batch sizes, device
+lanes (nkfs_gpu_set_devices), and the write-back contract (bytes outside the
+defined outputs keep the caller's contents).  Checked against the
+device-resident entry points and the pinned oracle, bit-exact.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from nkfs_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+SENT = 0xA5
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nkfs_amd import _lib
+    lib = _lib.lib()
+    assert lib.nk8_init() == 0
+    return lib
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def u64(x):
+    return int(x) & 0xFFFFFFFFFFFFFFFF
+
+
+def ragged_layout(sizes, n_slots, k, block_gap=0, part_gap=0):
+    from nkfs_amd import batch
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos = ppos = 0
+    for s, B in enumerate(sizes):
+        boff[s], poff[s] = pos, ppos
+        pos += int(B) + block_gap
+        ppos += n_slots * batch.part_pitch(int(B), k) + part_gap
+    return boff, poff, pos, ppos
+
+
+def scatter_pages(blocks, page_size, rng):
+    """Put each block's bytes into its own 4 KiB pages, laid out in a
+    shuffled arena (like core/upages.c's page arrays): returns the arena,
+    the page address list and each stripe's first page index."""
+    npg = [max(1, -(-len(b) // page_size)) for b in blocks]
+    total = sum(npg)
+    arena = np.full(total * page_size, SENT, np.uint8)
+    slots = rng.permutation(total)
+    base = arena.ctypes.data
+    pages = np.zeros(total, np.int64)
+    first = np.zeros(len(blocks), np.int64)
+    p = 0
+    for s, b in enumerate(blocks):
+        first[s] = p
+        for i in range(npg[s]):
+            slot = int(slots[p])
+            pages[p] = base + slot * page_size
+            chunk = b[i * page_size:(i + 1) * page_size]
+            arena[slot * page_size: slot * page_size + len(chunk)] = chunk
+            p += 1
+    return arena, pages, first
+
+
+def gather_pages(arena, pages, first, sizes, page_size):
+    base = arena.ctypes.data
+    out = []
+    for s, B in enumerate(sizes):
+        b = np.empty(int(B), np.uint8)
+        for i in range(-(-int(B) // page_size)):
+            off = int(pages[first[s] + i]) - base
+            n = min(page_size, int(B) - i * page_size)
+            b[i * page_size: i * page_size + n] = arena[off: off + n]
+        out.append(b)
+    return out
+
+
+# ---------------------------------------------------------------- GET, uniform
+
+@pytest.mark.parametrize("S,B,n,k,chunk,pitch_pad", [(3000, 4096, 4, 2, 0, 0), (200, 262144, 8, 5, 1 << 20, 0),
+                                                     (97, 70001, 6, 3, 300000, 13), (40, 30000, 16, 12, 0, 7)])
+def test_decode_host_round_trip(L, O, S, B, n, k, chunk, pitch_pad):
+    """nkfs_nk8_decode_host: the k survivors of every stripe (random subset,
+    random order) shipped from host memory rebuild each block bit-exact;
+    pitched output keeps the gap bytes; a stripe offered duplicate ids
+    (fewer than k distinct) returns -EINVAL and keeps its block bytes."""
+    from nkfs_amd import batch
+    rng = np.random.default_rng(S + B)
+    blocks = batch.synth(S, B, first=11)
+    ids_np = synth.batch_ids(S, n, first=11)
+    parts, _ = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    pitch = batch.part_pitch(B, k)
+    pn = parts.cpu().numpy().reshape(S, n, pitch)
+    # survivors: k random slots per stripe, packed as the caller holds them
+    pick = np.stack([rng.permutation(n)[:k] for _ in range(S)])
+    held = np.ascontiguousarray(pn[np.arange(S)[:, None], pick])          # [S, k, pitch]
+    hid = np.ascontiguousarray(ids_np[np.arange(S)[:, None], pick])       # [S, k]
+    avail = np.tile(np.arange(k, dtype=np.uint8), (S, 1))
+    bad = 5 % S
+    hid[bad, 1] = hid[bad, 0]  # duplicate id: fewer than k distinct
+    bp = B + pitch_pad
+    out = np.full(S * bp, SENT, np.uint8)
+    status = np.full(S, 99, np.int32)
+    rc = batch.decode_host(held.reshape(-1), pitch, k, hid.reshape(-1), avail.reshape(-1), k, k, B, out, bp,
+                           status=status, chunk_bytes=chunk)
+    assert rc == 0
+    want = blocks.cpu().numpy()[:, :B]
+    got = out.reshape(S, bp)
+    ok = np.ones(S, bool)
+    ok[bad] = False
+    assert status[bad] == -22 and (status[ok] == 0).all()
+    assert np.array_equal(got[ok, :B], want[ok])
+    assert (got[bad] == SENT).all()
+    if pitch_pad:
+        assert (got[:, B:] == SENT).all()
+    # one stripe through the oracle's assemble as well
+    s = 1
+    ob = O.decode([held[s, c, :batch.part_size(B, k)] for c in range(k)], hid[s], k, B)
+    assert np.array_equal(ob, want[s])
+
+
+def test_decode_host_verify(L):
+    """GET with the part check fused in (h_expect): a flipped byte in a
+    part that is used fails its stripe with -EIO and flags the slot."""
+    from nkfs_amd import batch
+    S, B, n, k = 300, 65536, 8, 5
+    blocks = batch.synth(S, B, first=77)
+    ids_np = synth.batch_ids(S, n, first=77)
+    parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    pitch = batch.part_pitch(B, k)
+    pn = parts.cpu().numpy().copy().reshape(-1)
+    dg = dig.cpu().numpy()
+    pn[(9 * n + 2) * pitch + 100] ^= 1
+    avail = np.tile(np.array([2, 0, 4, 6, 7, 1], np.uint8), (S, 1))
+    out = np.zeros(S * B, np.uint8)
+    status = np.zeros(S, np.int32)
+    badmask = np.zeros(S, np.int64)
+    assert batch.decode_host(pn, pitch, n, ids_np.reshape(-1), avail.reshape(-1), 6, k, B, out, B,
+                             status=status, expect=dg, badmask=badmask, chunk_bytes=4 << 20) == 0
+    assert status[9] == -5 and badmask[9] == 1 << 2
+    others = np.arange(S) != 9
+    assert (status[others] == 0).all() and (badmask[others] == 0).all()
+    assert np.array_equal(out.reshape(S, B)[others], blocks.cpu().numpy()[others, :B])
+
+
+# ---------------------------------------------------------------- ragged, gaps
+
+@pytest.mark.parametrize("n,k,chunk", [(8, 5, 0), (4, 2, 1 << 20), (6, 3, 100000)])
+def test_ragged_host_gaps_untouched(L, n, k, chunk):
+    """PUT and GET of a ragged batch whose block and part ranges have gaps
+    between stripes: parts/blocks equal the device-resident result and
+    every gap byte keeps the caller's sentinel (pipeline.c)."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(29)
+    sizes[:3] = (1048576, 1, 70001)
+    boff, poff, pos, ppos = ragged_layout(sizes, n, k, block_gap=24, part_gap=48)
+    host = np.full(pos, SENT, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(900 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=900)
+    parts_h = np.full(ppos, SENT, np.uint8)
+    dig_h = np.zeros(len(sizes) * n, np.int64)
+    batch.encode_ragged_host(host, boff, sizes.astype(np.int32), n, k, ids_np, parts_h, poff, dig_h,
+                             chunk_bytes=chunk)
+    parts_d = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    dig_d = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts_d, dev(poff),
+                        dig_d, int(sizes.max()))
+    torch.cuda.synchronize()
+    assert np.array_equal(dig_h, dig_d.cpu().numpy())
+    pd = parts_d.cpu().numpy()
+    inside = np.zeros(ppos, bool)
+    for s, B in enumerate(sizes):
+        pitch, ps = batch.part_pitch(int(B), k), batch.part_size(int(B), k)
+        inside[poff[s]: poff[s] + n * pitch] = True
+        for i in range(n):
+            a = poff[s] + i * pitch
+            assert np.array_equal(parts_h[a: a + ps], pd[a: a + ps]), (s, i)
+    assert (parts_h[~inside] == SENT).all()
+    # GET from every slot back into a sentinel-filled buffer with gaps
+    rng = np.random.default_rng(n)
+    avail = np.stack([rng.permutation(n) for _ in sizes]).astype(np.uint8)
+    out = np.full(pos, SENT, np.uint8)
+    status = np.full(len(sizes), 7, np.int32)
+    assert batch.decode_ragged_host(parts_h, poff, n, ids_np, avail, n, k, out, boff, sizes.astype(np.int32),
+                                    status=status, chunk_bytes=chunk) == 0
+    assert (status == 0).all()
+    blk = np.zeros(pos, bool)
+    for s, B in enumerate(sizes):
+        blk[boff[s]: boff[s] + B] = True
+    assert np.array_equal(out[blk], host[blk]) and (out[~blk] == SENT).all()
+
+
+# ---------------------------------------------------------------- page lists
+
+@pytest.mark.parametrize("n,k,chunk,page", [(8, 5, 0, 4096), (4, 2, 1 << 20, 4096), (6, 3, 200000, 512)])
+def test_pages_put_get(L, O, n, k, chunk, page):
+    """PUT from page lists (nkfs_nk8_encode_pages: each block spread over
+    pages in a shuffled arena, as core/upages.c holds a payload) equals the
+    device-resident ragged encode; GET back into fresh page lists
+    (nkfs_nk8_decode_pages) rebuilds every block; digests of a sample
+    against the oracle."""
+    from nkfs_amd import batch
+    rng = np.random.default_rng(page + n)
+    sizes = synth.mixed_sizes(26)
+    sizes[:4] = (1048576, 1, page, page + 1)
+    blocks = [synth.stripe_bytes(2000 + s, int(B)) for s, B in enumerate(sizes)]
+    arena, pages, first = scatter_pages(blocks, page, rng)
+    ids_np = synth.batch_ids(len(sizes), n, first=2000)
+    _, poff, _, ppos = ragged_layout(sizes, n, k, part_gap=16)
+    parts_h = np.full(ppos, SENT, np.uint8)
+    dig_h = np.zeros(len(sizes) * n, np.int64)
+    sz32 = sizes.astype(np.int32)
+    assert batch.encode_pages(pages, page, first, sz32, n, k, ids_np, parts_h, poff, dig_h, chunk_bytes=chunk) == 0
+    # reference: the same bytes packed, device-resident ragged encode
+    boff, _, pos, _ = ragged_layout(sizes, n, k)
+    packed = np.concatenate(blocks)
+    parts_d = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    dig_d = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+    batch.encode_ragged(dev(packed), dev(boff), dev(sz32), n, k, dev(ids_np), parts_d, dev(poff), dig_d,
+                        int(sizes.max()))
+    torch.cuda.synchronize()
+    assert np.array_equal(dig_h, dig_d.cpu().numpy())
+    pd = parts_d.cpu().numpy()
+    for s, B in enumerate(sizes):
+        pitch, ps = batch.part_pitch(int(B), k), batch.part_size(int(B), k)
+        for i in range(n):
+            a = poff[s] + i * pitch
+            assert np.array_equal(parts_h[a: a + ps], pd[a: a + ps]), (s, i)
+    for s in (2, 3):
+        want = [O.xxh64(p) for p in O.encode(blocks[s], n, k, ids_np[s])]
+        assert [u64(x) for x in dig_h[s * n:(s + 1) * n]] == want
+    # GET into fresh, differently shuffled pages (erase n-k slots per stripe)
+    arena2, pages2, first2 = scatter_pages([np.zeros(int(B), np.uint8) for B in sizes], page, rng)
+    arena2[:] = SENT
+    avail = np.stack([rng.permutation(n)[:k] for _ in sizes]).astype(np.uint8)
+    status = np.full(len(sizes), 3, np.int32)
+    assert batch.decode_pages(parts_h, poff, n, ids_np, avail, k, k, pages2, page, first2, sz32, status=status,
+                              chunk_bytes=chunk) == 0
+    assert (status == 0).all()
+    got = gather_pages(arena2, pages2, first2, sizes, page)
+    for s in range(len(sizes)):
+        assert np.array_equal(got[s], blocks[s]), s
+    # page tails past each block keep the sentinel
+    base = arena2.ctypes.data
+    for s, B in enumerate(sizes):
+        last = int(pages2[first2[s] + (int(B) - 1) // page]) - base
+        used = int(B) - ((int(B) - 1) // page) * page
+        assert (arena2[last + used: last + page] == SENT).all()
+
+
+# ---------------------------------------------------------------- device lanes
+
+def test_lanes_split_identical(L):
+    """nkfs_gpu_set_devices with several lanes (the same device repeated on
+    a one-GPU box, every visible device otherwise): the byte-balanced split
+    gives the same parts, digests and rebuilt blocks as one lane."""
+    from nkfs_amd import batch
+    ndev = L.nkfs_gpu_count()
+    lanes = [0, 0, 0] if ndev < 2 else list(range(min(ndev, 4)))
+    S, B, n, k = 1000, 65536, 8, 5
+    host = np.ascontiguousarray(batch.synth(S, B, first=3).cpu().numpy())
+    ids_np = synth.batch_ids(S, n, first=3)
+    ref_parts, ref_dig = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=4 << 20)
+    try:
+        assert batch.set_devices(lanes) == 0
+        assert batch.get_devices() == lanes
+        parts, dig = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=4 << 20)
+        assert torch.equal(parts[:, :batch.part_size(B, k)], ref_parts[:, :batch.part_size(B, k)])
+        assert torch.equal(dig, ref_dig)
+        out = np.zeros(S * B, np.uint8)
+        status = np.zeros(S, np.int32)
+        avail = np.tile(np.array([7, 6, 5, 4, 3], np.uint8), (S, 1))
+        assert batch.decode_host(parts.numpy().reshape(-1), batch.part_pitch(B, k), n, ids_np.reshape(-1),
+                                 avail.reshape(-1), k, k, B, out, B, status=status, chunk_bytes=4 << 20) == 0
+        assert (status == 0).all() and np.array_equal(out.reshape(S, B), host[:, :B])
+        # ragged, byte-balanced over the lanes
+        sizes = synth.mixed_sizes(300)
+        boff, poff, pos, ppos = ragged_layout(sizes, n, k)
+        hb = np.zeros(pos, np.uint8)
+        for s, Bs in enumerate(sizes):
+            hb[boff[s]: boff[s] + Bs] = synth.stripe_bytes(s, int(Bs))
+        rid = synth.batch_ids(len(sizes), n)
+        got = []
+        for ln in (lanes, []):
+            assert batch.set_devices(ln) == 0
+            ph = np.zeros(ppos, np.uint8)
+            dh = np.zeros(len(sizes) * n, np.int64)
+            batch.encode_ragged_host(hb, boff, sizes.astype(np.int32), n, k, rid, ph, poff, dh, chunk_bytes=8 << 20)
+            got.append((ph, dh))
+        defined = np.zeros(ppos, bool)  # part bytes (the pitch padding is unspecified)
+        for s, Bs in enumerate(sizes):
+            pitch, ps = batch.part_pitch(int(Bs), k), batch.part_size(int(Bs), k)
+            for i in range(n):
+                defined[poff[s] + i * pitch: poff[s] + i * pitch + ps] = True
+        assert np.array_equal(got[0][1], got[1][1])
+        assert np.array_equal(got[0][0][defined], got[1][0][defined])
+    finally:
+        batch.set_devices([])
+    assert batch.get_devices() == [L.nkfs_gpu_device()]
+
+
+def test_set_devices_rejects_missing(L):
+    from nkfs_amd import batch
+    assert batch.set_devices([L.nkfs_gpu_count()]) == -19  # -ENODEV
+    assert batch.get_devices() == [L.nkfs_gpu_device()]
+
+
+# ---------------------------------------------------------------- pin registry
+
+def test_concurrent_calls_share_pageable_buffer(L):
+    """Several threads run the host pipeline on the same pageable buffers
+    at once: the registration is reference counted, so no call unpins
+    memory another call is still copying (pipeline.c pin())."""
+    from nkfs_amd import batch
+    S, B, n, k = 600, 65536, 8, 5
+    host = np.ascontiguousarray(batch.synth(S, B, first=8).cpu().numpy())
+    ids_np = synth.batch_ids(S, n, first=8)
+    ref, ref_dig = batch.encode_host(host, B, n, k, ids_np)
+    errs = []
+
+    def work():
+        try:
+            for _ in range(3):
+                p, d = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=2 << 20)
+                assert torch.equal(d, ref_dig)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+
+
+def test_host_register_api(L):
+    buf = np.zeros(1 << 20, np.uint8)
+    p = buf.ctypes.data
+    assert L.nkfs_host_register(p, buf.nbytes) == 0
+    assert L.nkfs_host_register(p, buf.nbytes) == 0   # second reference
+    assert L.nkfs_host_unregister(p) == 0
+    assert L.nkfs_host_unregister(p) == 0
+    assert L.nkfs_host_unregister(p) == -2            # -ENOENT: released
+    pinned = torch.empty(4096, dtype=torch.uint8, pin_memory=True)
+    assert L.nkfs_host_register(pinned.data_ptr(), 4096) == -17  # -EEXIST: runtime-pinned
+
+
+# ---------------------------------------------------------------- general path, big parts
+
+def test_generic_parts_beyond_grid_y(L, O):
+    """n > 8 with parts past 16 MiB: the general kernels grid-stride over
+    rows beyond 65,535 x 256.  Round trip, and part bytes at
+    rows past that limit against the GF product table."""
+    from nkfs_amd import batch
+    n, k = 10, 9
+    B = 9 * (17 << 20) + 5
+    blocks = batch.synth(1, B, first=4)
+    ids_np = np.array([[3, 9, 27, 81, 243, 1, 2, 4, 8, 16]], np.uint8)
+    parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    mul = O.gf_mul_table()
+    blk = blocks[0, :B].cpu().numpy()
+    pn = parts.cpu().numpy()
+    for j in (0, 65535 * 256 + 3, ps - 1):
+        row = np.zeros(k, np.uint8)
+        seg = blk[j * k: j * k + k]
+        row[:len(seg)] = seg
+        for i in range(n):
+            c, acc = 1, 0
+            for m in range(k):
+                acc ^= int(mul[c, row[m]])
+                c = int(mul[c, ids_np[0, i]])
+            assert pn[i, j] == acc, (i, j)
+    avail = dev(np.array([[9, 7, 5, 3, 1, 0, 2, 4, 6]], np.uint8))
+    out, st = batch.decode(parts, n, dev(ids_np), avail, k, B)
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0 and torch.equal(out[0, :B], blocks[0, :B])
