@@ -320,24 +320,11 @@ def run_ragged(args, rank, world, device, steps):
         pos += (B + 255) // 256 * 256
         ppos += n * batch.part_pitch(B, k)
     stream = torch.cuda.current_stream(device)
-    # stripes generated on the device per size class (synth stripe = global
-    # stripe index), scattered into the packed buffer in 256-byte rows: a
-    # few launches, not one per stripe
+    # every stripe generated on the device in one launch (synth stripe =
+    # global stripe index)
     blocks = torch.zeros(pos, dtype=torch.uint8, device=device)
-    rows = blocks.view(-1, 256)
-    for B in C5_SIZES:
-        idx = np.nonzero(sizes == B)[0]
-        if not len(idx):
-            continue
-        # consecutive runs of global ids of this class, each synthesised at once
-        gid = idx + lo
-        cuts = np.nonzero(np.diff(gid) != 1)[0] + 1
-        for run in np.split(np.arange(len(idx)), cuts):
-            data = batch.synth(len(run), B, first=int(gid[run[0]]), device=device)
-            r = (torch.from_numpy(boff[idx[run]] // 256).to(device)[:, None] +
-                 torch.arange(B // 256, device=device)[None, :]).reshape(-1)
-            rows[r] = data[:, :B].reshape(-1, 256)
-            del data, r
+    batch.synth_ragged(blocks, torch.from_numpy(boff).to(device), torch.from_numpy(sizes.astype(np.int32)).to(device),
+                       first=lo, stream=stream)
     ids_np = synth.batch_ids(S, n, first=lo)
     ids = torch.from_numpy(ids_np).to(device)
     avail = torch.from_numpy(synth.batch_survivors(S, n, k, first=lo)).to(device)

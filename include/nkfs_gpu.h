@@ -273,6 +273,13 @@ int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch,
 		      uint32_t block_size, uint32_t nstripes, uint64_t seed,
 		      uint64_t first_stripe, void *stream);
 
+/* The same stripes for a ragged layout in one launch: stripe s (stripe
+ * index first_stripe + s) is d_block_size[s] bytes at d_blocks +
+ * d_block_off[s]. */
+int nkfs_synth_ragged(uint8_t *d_blocks, const uint64_t *d_block_off,
+		      const uint32_t *d_block_size, uint32_t nstripes, uint64_t seed,
+		      uint64_t first_stripe, void *stream);
+
 /* Device memory helpers for callers without their own allocator. */
 void *nkfs_dev_alloc(size_t bytes);
 void nkfs_dev_free(void *d_ptr);

@@ -93,6 +93,7 @@ _SIGS = {
     "nkfs_gpu_count": (C.c_int, []),
     "nkfs_gpu_set_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "nkfs_gpu_get_devices": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
+    "nkfs_synth_ragged": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint64, vp]),
     "nkfs_synth_blocks": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, vp]),
     "nkfs_dev_alloc": (vp, [C.c_size_t]),
     "nkfs_dev_free": (None, [vp]),

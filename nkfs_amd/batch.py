@@ -335,6 +335,19 @@ def synth(nstripes: int, block_size: int, pitch: int | None = None, seed: int | 
     return t
 
 
+def synth_ragged(blocks: torch.Tensor, block_off: torch.Tensor, block_sizes: torch.Tensor, seed: int | None = None,
+                 first: int = 0, stream=None) -> torch.Tensor:
+    """Fill a packed ragged batch in place (one launch): stripe s = the
+    synthetic stripe first + s, block_sizes[s] bytes at block_off[s]."""
+    from .synth import SEED
+    _need(blocks, U8, "blocks")
+    _need(block_off, torch.int64, "block_off")
+    _need(block_sizes, torch.int32, "block_sizes")
+    check(lib().nkfs_synth_ragged(blocks.data_ptr(), block_off.data_ptr(), block_sizes.data_ptr(), block_sizes.numel(),
+                                  SEED if seed is None else seed, first, _stream(stream)), "nkfs_synth_ragged")
+    return blocks
+
+
 def digests_u64(d: torch.Tensor):
     """int64 digest tensor -> list of Python unsigned ints."""
     return [v & 0xFFFFFFFFFFFFFFFF for v in d.cpu().tolist()]

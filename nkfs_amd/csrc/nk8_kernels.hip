@@ -244,10 +244,23 @@ __global__ __launch_bounds__(64) void k_xxh64_stripes(u64 *state_v, const u8 *da
             b[li * 4 + q] = w[q];
         __syncthreads();
         load(p + 1);  // in flight under this piece's rounds
-        const u64 cnt = nst - p * 64 < 64 ? nst - p * 64 : 64;
-        if (li < 4)
-            for (u64 r = 0; r < cnt; ++r)
+        const u32 cnt = u32(nst - p * 64 < 64 ? nst - p * 64 : 64);
+        if (li < 4) {
+            // 8 rounds per group, their words read together: the serial
+            // chain never waits on an LDS read
+            u32 r = 0;
+            for (; r + 8 <= cnt; r += 8) {
+                u64 wv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    wv[j] = b[(r + j) * 4 + a];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    acc = xxh_round(acc, wv[j]);
+            }
+            for (; r < cnt; ++r)
                 acc = xxh_round(acc, b[r * 4 + a]);
+        }
     }
     if (li < 4)
         state_v[a] = acc;
@@ -478,6 +491,28 @@ __global__ __launch_bounds__(256) void k_synth(u8 *blocks, u64 pitch, u32 B, u32
     }
 }
 
+// Ragged form: one workgroup per stripe s, d_block_size[s] bytes at
+// d_block_off[s], stripe index first + s (the same bytes k_synth gives that
+// stripe).
+__global__ __launch_bounds__(256) void k_synth_ragged(u8 *blocks, const u64 *boff, const u32 *bsize, u64 seed,
+                                                      u64 first)
+{
+    const u64 s = blockIdx.x;
+    const u32 B = bsize[s];
+    u8 *dst0 = blocks + boff[s];
+    const u32 nw = (B + 7) / 8;
+    for (u32 w = threadIdx.x; w < nw; w += blockDim.x) {
+        const u64 val = mix64(seed + 0x9E3779B97F4A7C15ull * (((first + s) << 32) + w + 1));
+        u8 *dst = dst0 + u64(w) * 8;
+        if (w * 8 + 8 <= B && (reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+            *reinterpret_cast<u64 *>(dst) = val;
+            continue;
+        }
+        for (u32 b = 0; b < 8 && w * 8 + b < B; ++b)
+            dst[b] = u8(val >> (8 * b));
+    }
+}
+
 // ----------------------------------------------------------- launchers
 
 extern "C" int nkfs_fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int rules, int nib, hipStream_t st);
@@ -585,6 +620,17 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
     return nkfs_fast_encode(g, ids, digests, kern == NKFS_ENC_AUTO, t.enc_nib, st);
 }
 
+// A handful of big stripes (the drop-in nk8_split_block: one block per
+// call) would leave the fast kernels' one wave per stripe alone on the chip;
+// the general kernel spreads every stripe's rows over the whole GPU (1 MiB
+// N8K5 split: 855 -> see DESIGN.md §5, per-call table).
+static bool few_big_stripes(const nkfs_geom *g)
+{
+    const u32 ps = max_part_size(g, g->block_size);
+    return !g->block_sizes && nkfs_g_tune.enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
+           g->nstripes < 64 && ps >= 8192;
+}
+
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
                                   void *stream)
 {
@@ -592,7 +638,7 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         return 0;
     hipStream_t st = (hipStream_t)stream;
     int rc = -ENOSYS;
-    if (g->n <= 8 && g->k <= 8 && nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC) {
+    if (g->n <= 8 && g->k <= 8 && nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC && !few_big_stripes(g)) {
         rc = with_size_order(g, st, [&](const nkfs_geom *go) { return fast_encode(go, ids, digests, st); });
         if (rc == -ENOSYS)
             rc = fast_encode(g, ids, digests, st);
@@ -700,6 +746,16 @@ extern "C" int nkfs_launch_synth(uint8_t *blocks, uint64_t pitch, uint32_t B, ui
     const u64 total = u64((B + 7) / 8) * nstripes;
     const u32 grid = u32(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
     hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, (hipStream_t)stream, blocks, pitch, B, nstripes, seed,
+                       first);
+    return launch_ok();
+}
+
+extern "C" int nkfs_launch_synth_ragged(uint8_t *blocks, const uint64_t *boff, const uint32_t *bsize,
+                                        uint32_t nstripes, uint64_t seed, uint64_t first, void *stream)
+{
+    if (!nstripes)
+        return 0;
+    hipLaunchKernelGGL(k_synth_ragged, dim3(nstripes), dim3(256), 0, (hipStream_t)stream, blocks, boff, bsize, seed,
                        first);
     return launch_ok();
 }

@@ -72,6 +72,8 @@ int nkfs_fast_xxh64_pages(const uint8_t *const *pages, const uint64_t *first,
 int nkfs_launch_synth(uint8_t *blocks, uint64_t block_pitch,
 		      uint32_t block_size, uint32_t nstripes,
 		      uint64_t seed, uint64_t first_stripe, void *stream);
+int nkfs_launch_synth_ragged(uint8_t *blocks, const uint64_t *block_off, const uint32_t *block_size,
+			     uint32_t nstripes, uint64_t seed, uint64_t first_stripe, void *stream);
 
 /* Part pitch used when the library lays parts out itself (ragged batches,
  * the drop-in entry points): part_size rounded up to whole 256-byte spans so

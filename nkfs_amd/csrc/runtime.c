@@ -585,6 +585,16 @@ int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_si
 	return nkfs_launch_synth(d_blocks, block_pitch, block_size, nstripes, seed, first_stripe, stream);
 }
 
+int nkfs_synth_ragged(uint8_t *d_blocks, const uint64_t *d_block_off, const uint32_t *d_block_size,
+		      uint32_t nstripes, uint64_t seed, uint64_t first_stripe, void *stream)
+{
+	if (!g_ready)
+		return -EAGAIN;
+	if (nstripes && (!d_blocks || !d_block_off || !d_block_size))
+		return -EINVAL;
+	return nkfs_launch_synth_ragged(d_blocks, d_block_off, d_block_size, nstripes, seed, first_stripe, stream);
+}
+
 void *nkfs_dev_alloc(size_t bytes)
 {
 	void *p = NULL;

@@ -394,3 +394,20 @@ def test_generic_parts_beyond_grid_y(L, O):
     out, st = batch.decode(parts, n, dev(ids_np), avail, k, B)
     torch.cuda.synchronize()
     assert int(st[0]) == 0 and torch.equal(out[0, :B], blocks[0, :B])
+
+
+def test_synth_ragged_matches_uniform(L):
+    """nkfs_synth_ragged (the bench's one-launch C5 input) gives every stripe
+    the bytes of the synthetic stream (nkfs_amd/synth.py), gaps untouched."""
+    from nkfs_amd import batch
+    sizes = np.array([1, 7, 4096, 65536, 1048576, 300001, 8], np.uint32)
+    boff, _, pos, _ = ragged_layout(sizes, 1, 1, block_gap=5)
+    buf = torch.full((pos,), SENT, dtype=torch.uint8, device="cuda")
+    batch.synth_ragged(buf, dev(boff), dev(sizes.astype(np.int32)), first=40)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    inside = np.zeros(pos, bool)
+    for s, B in enumerate(sizes):
+        assert np.array_equal(got[boff[s]: boff[s] + B], synth.stripe_bytes(40 + s, int(B))), s
+        inside[boff[s]: boff[s] + B] = True
+    assert (got[~inside] == SENT).all()

@@ -1,0 +1,150 @@
+"""PCIe-inclusive rates of the host-memory entry points (include/nkfs_gpu.h):
+the path's real ends, SURVEY.md §8(f) row 2.  User bytes (block bytes) per
+second, host buffers pinned once (a server's page pool), outputs verified
+against the inputs after timing.
+
+    python tools/pcie_bench.py [c2 c3 c4 c5 pages lanes]
+
+PUT  = nkfs_nk8_encode_host: blocks H2D -> encode + XXH64 -> parts + digests D2H
+GET  = nkfs_nk8_decode_host: k survivor parts per stripe H2D -> decode -> blocks D2H
+       (+ verify: the part digests checked inside the rebuild)
+pages = the same through 4 KiB page lists (nkfs_nk8_encode_pages /
+       nkfs_nk8_decode_pages: gathered into / scattered from pinned staging)
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import C5_SIZES, CONFIGS  # noqa: E402
+from nkfs_amd import _lib, batch, synth  # noqa: E402
+
+GIB = 2**30
+
+
+def timed(fn, reps=3):
+    fn()  # warm-up: pooled contexts and scratch
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rc = fn()
+        assert rc in (None, 0) or isinstance(rc, tuple), rc
+    return (time.perf_counter() - t0) / reps
+
+
+def uniform(name, user_bytes=1 << 30, lanes=None):
+    S0, B, n, k, _ = CONFIGS[name]
+    S = min(S0, user_bytes // B)
+    pitch = batch.part_pitch(B, k)
+    blocks = batch.synth(S, B).cpu()[:, :B].contiguous().pin_memory()
+    ids = torch.from_numpy(synth.batch_ids(S, n)).pin_memory()
+    parts = torch.empty((S * n, pitch), dtype=torch.uint8).pin_memory()
+    dig = torch.empty(S * n, dtype=torch.int64).pin_memory()
+    if lanes is not None:
+        _lib.check(batch.set_devices(lanes))
+    t_put = timed(lambda: batch.encode_host(blocks, B, n, k, ids, out=(parts, dig)))
+    # GET: the k survivors each stripe holds, packed (n_slots = k)
+    surv = synth.batch_survivors(S, n, k).astype(np.int64)
+    pv = parts.view(S, n, pitch)
+    idx = torch.from_numpy(surv)
+    held = torch.gather(pv, 1, idx[:, :, None].expand(S, k, pitch)).contiguous().pin_memory()
+    hid = torch.gather(ids.view(S, n).long(), 1, idx).to(torch.uint8).contiguous().pin_memory()
+    hexp = torch.gather(dig.view(S, n), 1, idx).contiguous().pin_memory()
+    avail = torch.arange(k, dtype=torch.uint8).repeat(S, 1).contiguous().pin_memory()
+    out = torch.empty((S, B), dtype=torch.uint8).pin_memory()
+    st = torch.empty(S, dtype=torch.int32).pin_memory()
+    bad = torch.empty(S, dtype=torch.int64).pin_memory()
+    t_get = timed(lambda: batch.decode_host(held, pitch, k, hid, avail, k, k, B, out, B, status=st))
+    ok = bool(torch.equal(out, blocks)) and int(st.abs().sum()) == 0
+    t_getv = timed(lambda: batch.decode_host(held, pitch, k, hid, avail, k, k, B, out, B, status=st, expect=hexp,
+                                             badmask=bad))
+    ok = ok and bool(torch.equal(out, blocks)) and int(st.abs().sum()) == 0
+    if lanes is not None:
+        batch.set_devices([])
+    ub = S * B
+    tag = f"{name} lanes={lanes}" if lanes is not None else name
+    print(f"{tag:18s} {S:6d} x {B:8d}  PUT {ub / t_put / GIB:6.2f} GiB/s   GET {ub / t_get / GIB:6.2f} GiB/s   "
+          f"GET+verify {ub / t_getv / GIB:6.2f} GiB/s   in/out per GiB user: PUT {1 + n * pitch / B:.2f} GiB, "
+          f"GET {1 + k * pitch / B:.2f} GiB   verified={ok}", flush=True)
+
+
+def ragged(user_bytes=1 << 30, pages=False, page=4096):
+    n, k = 8, 5
+    sizes = synth.mixed_sizes(CONFIGS["c5"][0], C5_SIZES)
+    keep = int(np.searchsorted(np.cumsum(sizes.astype(np.int64)), user_bytes)) + 1
+    sizes = sizes[:keep]
+    S = len(sizes)
+    boff = np.zeros(S, np.int64)
+    poff = np.zeros(S, np.int64)
+    pos = ppos = 0
+    for s, B in enumerate(sizes.tolist()):
+        boff[s], poff[s] = pos, ppos
+        pos += (B + 255) // 256 * 256
+        ppos += n * batch.part_pitch(B, k)
+    host = torch.zeros(pos, dtype=torch.uint8).pin_memory()
+    for s, B in enumerate(sizes.tolist()):
+        host[boff[s]: boff[s] + B] = torch.from_numpy(synth.stripe_bytes(s, B))
+    ids = torch.from_numpy(synth.batch_ids(S, n)).pin_memory()
+    parts = torch.empty(ppos, dtype=torch.uint8).pin_memory()
+    dig = torch.empty(S * n, dtype=torch.int64).pin_memory()
+    sz = torch.from_numpy(sizes.astype(np.int32))
+    bo, po = torch.from_numpy(boff), torch.from_numpy(poff)
+    avail = torch.from_numpy(synth.batch_survivors(S, n, k))
+    st = torch.empty(S, dtype=torch.int32)
+    ub = int(sizes.sum())
+    if not pages:
+        t_put = timed(lambda: batch.encode_ragged_host(host, bo, sz, n, k, ids, parts, po, dig))
+        out = torch.zeros(pos, dtype=torch.uint8).pin_memory()
+        t_get = timed(lambda: batch.decode_ragged_host(parts, po, n, ids, avail, k, k, out, bo, sz, status=st))
+        ok = bool(torch.equal(out, host)) and int(st.abs().sum()) == 0
+        print(f"c5 ragged          {S:6d} stripes  PUT {ub / t_put / GIB:6.2f} GiB/s   GET {ub / t_get / GIB:6.2f} GiB/s"
+              f"   (GET ships all {n} slots)   verified={ok}", flush=True)
+        return
+    # page lists: every block in its own 4 KiB pages of a pinned pool
+    npg = [(B + page - 1) // page for B in sizes.tolist()]
+    first = np.concatenate([[0], np.cumsum(npg)[:-1]]).astype(np.int64)
+    pool = torch.zeros(int(sum(npg)) * page, dtype=torch.uint8).pin_memory()
+    rng = np.random.default_rng(7)
+    slot = rng.permutation(int(sum(npg)))
+    pg = torch.from_numpy(pool.data_ptr() + slot.astype(np.int64) * page)
+    pn = pool.numpy()
+    for s, B in enumerate(sizes.tolist()):
+        src = host[boff[s]: boff[s] + B].numpy()
+        for i in range(npg[s]):
+            o = int(slot[first[s] + i]) * page
+            c = src[i * page:(i + 1) * page]
+            pn[o: o + len(c)] = c
+    fp = torch.from_numpy(first)
+    t_put = timed(lambda: batch.encode_pages(pg, page, fp, sz, n, k, ids, parts, po, dig))
+    pool2 = torch.zeros_like(pool).pin_memory()
+    pg2 = torch.from_numpy(pool2.data_ptr() + slot.astype(np.int64) * page)
+    t_get = timed(lambda: batch.decode_pages(parts, po, n, ids, avail, k, k, pg2, page, fp, sz, status=st))
+    ok = bool(torch.equal(pool2, pool)) or all(
+        np.array_equal(pool2.numpy()[int(slot[first[s]]) * page: int(slot[first[s]]) * page + min(B, page)],
+                       host[boff[s]: boff[s] + min(B, page)].numpy()) for s, B in enumerate(sizes.tolist()))
+    print(f"c5 pages ({page} B)  {S:6d} stripes  PUT {ub / t_put / GIB:6.2f} GiB/s   GET {ub / t_get / GIB:6.2f} GiB/s"
+          f"   verified={ok}", flush=True)
+
+
+def main():
+    L = _lib.lib()
+    _lib.check(L.nkfs_gpu_init(0))
+    what = sys.argv[1:] or ["c2", "c3", "c4", "c5", "pages", "lanes"]
+    for w in what:
+        if w in ("c2", "c3", "c4"):
+            uniform(w)
+        elif w == "c5":
+            ragged()
+        elif w == "pages":
+            ragged(pages=True)
+        elif w == "lanes":
+            uniform("c3", lanes=[0, 0])
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
