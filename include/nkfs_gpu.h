@@ -69,6 +69,8 @@ struct nkfs_tune {
 	int enc_units;        /* walk encoder: 1,024-row units per chunk (0 auto, 1, 2; n <= 4 only) */
 	int size_order;       /* ragged batches run largest stripe first (0/1) */
 	int enc_prefetch;     /* walk encoder: chunks of loads in flight ahead of the one encoded (1, 2) */
+	int enc_fused_waves_per_cu; /* fused encoder: resident waves per CU cap (0 = none, 3..32) */
+	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
 };
 void nkfs_tune_get(struct nkfs_tune *t);
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields */

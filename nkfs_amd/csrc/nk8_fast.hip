@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "../../include/nkfs_gpu.h"
 #include "nk8_dev.h"
 #include "gf256.h"
 #include "nkfs_internal.h"
@@ -293,15 +294,34 @@ __global__ __launch_bounds__(64) void k_encode_fast(nkfs_geom g, const u8 *ids, 
     }
 }
 
+// Dynamic LDS request that caps a one-wave-workgroup kernel at `target`
+// resident waves per CU (0 = no cap): the LDS a CU has divided by the target,
+// less the kernel's static LDS.
+static size_t lds_cap_pad(const void *kern, int target)
+{
+    if (target <= 0)
+        return 0;
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, kern) != hipSuccess)
+        return 0;
+    if (target < 3)
+        target = 3;  // keeps the request under the 64 KiB dynamic default
+    const size_t per = size_t(160 * 1024) / size_t(target);
+    return per > a.sharedSizeBytes ? per - a.sharedSizeBytes : 0;
+}
+
 template <int E, bool HASH, bool NIB>
 static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig)
 {
     constexpr int G = E == 4 ? 4 : 2;
     const dim3 grid((g.nstripes + G - 1) / G);
+    const int cap = nkfs_g_tune.enc_fused_waves_per_cu;
     switch (k) {
 #define NKFS_K(KK)                                                                                      \
     case KK:                                                                                            \
-        hipLaunchKernelGGL((k_encode_fast<KK, E, 1, HASH, NIB>), grid, dim3(64), 0, st, g, ids, dig, false); \
+        hipLaunchKernelGGL((k_encode_fast<KK, E, 1, HASH, NIB>), grid, dim3(64),                        \
+                           lds_cap_pad(reinterpret_cast<const void *>(&k_encode_fast<KK, E, 1, HASH, NIB>), cap), \
+                           st, g, ids, dig, false);                                                      \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -773,14 +793,19 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     while (!verify && groups * slices < target && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
+    const int cap = nkfs_g_tune.dec_wave_waves_per_cu;
 #define NKFS_DK(KK, EE, GG)                                                                                       \
     do {                                                                                                          \
         if (verify)                                                                                               \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, true>), grid, dim3(64), 0, st, *g, n_slots, ids,      \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 1, true>), grid, dim3(64),                               \
+                               lds_cap_pad(reinterpret_cast<const void *>(&k_decode_fast<KK, EE, GG, 1, true>), cap), \
+                               st, *g, n_slots, ids, avail, navail, status, t->inv, nt, int(slices), expect,      \
+                               badmask);                                                                          \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64), 0, st, *g, n_slots, ids,     \
-                               avail, navail, status, t->inv, nt, int(slices), expect, badmask);                  \
+            hipLaunchKernelGGL((k_decode_fast<KK, EE, GG, 2, false>), grid, dim3(64),                              \
+                               lds_cap_pad(reinterpret_cast<const void *>(&k_decode_fast<KK, EE, GG, 2, false>), cap), \
+                               st, *g, n_slots, ids, avail, navail, status, t->inv, nt, int(slices), expect,      \
+                               badmask);                                                                          \
     } while (0)
     switch (g->k) {
     case 2: NKFS_DK(2, 4, 1); break;

@@ -324,6 +324,86 @@ static void page_copy(const struct hp *h, uint32_t s, uint8_t *buf, int to_pages
 	}
 }
 
+/* Gather (to_pages 0) or scatter (1) the blocks of stripes [s0, s1) between
+ * their page lists and the packed staging `buf` (block s at its packed
+ * 256-byte-aligned offset), stripes with skip[s - s0] set left alone.  A
+ * few host threads share the stripes: one memcpy stream tops out near
+ * 10 GB/s, below what PCIe moves. */
+#define COPY_THREADS 4
+
+struct pcopy {
+	const struct hp *h;
+	uint32_t s0, s1;
+	uint8_t *buf;
+	const uint64_t *off; /* packed offset of each stripe in [s0, s1) */
+	const int32_t *status;
+	int to_pages;
+};
+
+static void *pcopy_run(void *arg)
+{
+	const struct pcopy *c = arg;
+	for (uint32_t s = c->s0; s < c->s1; s++)
+		if (!c->status || c->status[s] != -EINVAL)
+			page_copy(c->h, s, c->buf + c->off[s], c->to_pages);
+	return NULL;
+}
+
+static void pages_copy(const struct hp *h, uint32_t s0, uint32_t s1, uint8_t *buf, const int32_t *status,
+		       int to_pages)
+{
+	const uint32_t cnt = s1 - s0;
+	uint64_t *off = malloc((size_t)cnt * sizeof(*off));
+	if (!off) { /* no scratch: one thread, offsets on the fly */
+		uint64_t o = 0;
+		for (uint32_t s = s0; s < s1; s++) {
+			if (!status || status[s - s0] != -EINVAL)
+				page_copy(h, s, buf + o, to_pages);
+			o += align256(hp_B(h, s));
+		}
+		return;
+	}
+	uint64_t o = 0, total = 0;
+	for (uint32_t s = 0; s < cnt; s++) {
+		off[s] = o;
+		o += align256(hp_B(h, s0 + s));
+	}
+	total = o;
+	int nt = total >= (4u << 20) ? COPY_THREADS : 1;
+	if ((uint32_t)nt > cnt)
+		nt = (int)cnt;
+	struct pcopy pc[COPY_THREADS];
+	pthread_t th[COPY_THREADS];
+	int started[COPY_THREADS] = {0};
+	/* byte-balanced contiguous stripe ranges, indices relative to s0 */
+	uint32_t a = 0;
+	for (int i = 0; i < nt; i++) {
+		const uint64_t goal = total * (uint64_t)(i + 1) / (uint64_t)nt;
+		uint32_t b = a;
+		while (b < cnt && (i == nt - 1 || off[b] < goal || b == a))
+			b++;
+		pc[i] = (struct pcopy){ h, a, b, buf, off, status, to_pages };
+		a = b;
+	}
+	/* pcopy_run indexes stripes relative to s0: shift the page lists */
+	struct hp hs = *h;
+	hs.first_page = h->first_page + s0;
+	if (h->sizes)
+		hs.sizes = h->sizes + s0;
+	for (int i = 0; i < nt; i++)
+		pc[i].h = &hs;
+	for (int i = 1; i < nt; i++)
+		started[i] = pthread_create(&th[i], NULL, pcopy_run, &pc[i]) == 0;
+	pcopy_run(&pc[0]);
+	for (int i = 1; i < nt; i++) {
+		if (started[i])
+			pthread_join(th[i], NULL);
+		else
+			pcopy_run(&pc[i]);
+	}
+	free(off);
+}
+
 #define HIPGO(call, what)                                              \
 	do {                                                           \
 		hipError_t e_ = (call);                                \
@@ -388,11 +468,10 @@ static int issue(const struct hp *h, struct ctxs *x)
 	/* payload in */
 	if (h->dir == HP_ENC) {
 		if (paged) {
+			pages_copy(h, u->s0, u->s1, hb + L->h_stage, NULL, 0);
 			uint64_t o = 0;
-			for (uint32_t s = u->s0; s < u->s1; s++) {
-				page_copy(h, s, hb + L->h_stage + o, 0);
-				o += h->sizes ? align256(hp_B(h, s)) : align256(h->block_size);
-			}
+			for (uint32_t s = u->s0; s < u->s1; s++)
+				o += align256(hp_B(h, s));
 			HIPGO(hipMemcpyAsync(d + L->d_blk, hb + L->h_stage, o, hipMemcpyHostToDevice, st),
 			      "H2D (gathered pages)");
 		} else {
@@ -538,14 +617,8 @@ static int retire(const struct hp *h, struct ctxs *x)
 			memcpy(h->status + u->s0, stv, (size_t)cnt * 4);
 		if (h->badmask)
 			memcpy(h->badmask + u->s0, x->hb + x->L.h_bad, (size_t)cnt * 8);
-		if (hp_paged(h)) {
-			uint64_t packed = 0;
-			for (uint32_t s = u->s0; s < u->s1; s++) {
-				if (stv[s - u->s0] != -EINVAL)
-					page_copy(h, s, x->hb + x->L.h_stage + packed, 1);
-				packed += align256(hp_B(h, s));
-			}
-		}
+		if (hp_paged(h))
+			pages_copy(h, u->s0, u->s1, x->hb + x->L.h_stage, stv, 1);
 	}
 out:
 	x->u.live = 0;

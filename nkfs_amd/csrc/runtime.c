@@ -54,6 +54,8 @@ struct nkfs_tune nkfs_g_tune = {
 	.enc_units = 0,
 	.size_order = 1,
 	.enc_prefetch = 1,
+	.enc_fused_waves_per_cu = 0,
+	.dec_wave_waves_per_cu = 0,
 };
 
 void nkfs_tune_get(struct nkfs_tune *t)
@@ -69,7 +71,9 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||
-	    (t->size_order != 0 && t->size_order != 1) || t->enc_prefetch < 1 || t->enc_prefetch > 2)
+	    (t->size_order != 0 && t->size_order != 1) || t->enc_prefetch < 1 || t->enc_prefetch > 2 ||
+	    (t->enc_fused_waves_per_cu && (t->enc_fused_waves_per_cu < 3 || t->enc_fused_waves_per_cu > 32)) ||
+	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)))
 		return -EINVAL;
 	nkfs_g_tune = *t;
 	return 0;

@@ -28,9 +28,18 @@ def main():
     ids = torch.from_numpy(synth.batch_ids(S, n)).cuda()
     parts = torch.empty((S * n, batch.part_pitch(B, k)), dtype=torch.uint8, device="cuda")
     dig = torch.empty(S * n, dtype=torch.int64, device="cuda")
+    ps = batch.part_size(B, k)
     with _lib.tuned(**{a: int(b) for a, b in kv.items()}):
-        for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for i in range(reps):
+            if i == 1:
+                ev[0].record()
             batch.encode(blocks, B, n, k, ids, parts, False if "nohash" in flags else dig)
+        ev[1].record()
+        torch.cuda.synchronize()
+        if reps > 1:
+            t = ev[0].elapsed_time(ev[1]) / 1e3 / (reps - 1)
+            print(f"{name} S={S} {kv} {sorted(flags)} encode {S * (B + n * ps + 8 * n) / t / 1e9:.0f} GB/s", flush=True)
         if "dec" in flags:
             avail = torch.from_numpy(synth.batch_survivors(S, n, k)).cuda()
             out = torch.empty((S, B), dtype=torch.uint8, device="cuda")
