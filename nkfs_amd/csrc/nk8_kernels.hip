@@ -593,7 +593,7 @@ static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
 {
     // uniform n > 4 batches of 32-128 KiB parts on grids beyond 2,048 fused
     // waves (C4: 16,384 x 256 KiB): the walk encoder, 4.75-4.93 -> 4.89-5.14
-    // TB/s across boxes (profiles/r02/ab_walk_encoder.txt); 1 MiB stripes stay
+    // TB/s across boxes (profiles/r02/ab_experiments.txt); 1 MiB stripes stay
     // on the warp-specialised kernel (C3: walk 4.99-5.03, ws 5.08-5.15)
     if (g->block_sizes || !digests || g->n <= 4)
         return 0;
