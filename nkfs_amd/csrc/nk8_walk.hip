@@ -209,18 +209,22 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
     using Buf = u32[U][4 * K];
     auto load_task = [&](Buf &x, u32 t, u32 j, u32 c) {
         const bool ok = task_ok(t, j);
-        // num_records rounded up to a dword: the buffer unit range-checks whole
-        // dwords (a dword straddling num_records reads 0); bytes past B in it
-        // are masked below (a dword never crosses a page, so it is mapped).
-        // The base is formed even for a task past the end: its offsets are
-        // all out of range, so nothing is read.
-        const __amdgpu_buffer_rsrc_t r = rsrc(blk_of(stripe_of(j)), (B + 3u) & ~3u);
+        // The resource starts at the chunk and spans the stripe's remaining
+        // bytes (scalar work per task); the lane offsets are loop-invariant,
+        // so no per-task VALU address temps exist for the compiler to fence
+        // with a wait before the loads issue.  num_records is rounded up to a
+        // dword: the buffer unit range-checks whole dwords (a dword
+        // straddling num_records reads 0); bytes past B in it are masked
+        // below (a dword never crosses a page, so it is mapped).  A task
+        // past the end gets num_records 0: nothing is read.
         const u32 cb = c * u32(R * K);
+        const u32 left = ok && B > cb ? ((B - cb + 3u) & ~3u) : 0u;
+        const __amdgpu_buffer_rsrc_t r = rsrc(blk_of(stripe_of(j)) + cb, left);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int q = 0; q < K; ++q) {
-                const u32 off = live_off(ok, cb + u32((u * 1024 + 16 * li) * K + 16 * q));
+                const u32 off = u32((u * 1024 + 16 * li) * K + 16 * q);
                 const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
                 x[u][4 * q] = v.x;
                 x[u][4 * q + 1] = v.y;
