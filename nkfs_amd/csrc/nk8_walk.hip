@@ -641,34 +641,47 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
         const u32 r0 = ru + 16 * li;
         u32 o[4 * K];
         if (r0 < ps) {
-            u32 tdep = 0;
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                u32 row[4 * W];
+            // the K lookups of each of a 4-row group's rows issued together,
+            // one group ahead of the XORs that consume them (up to 8K LDS
+            // reads in flight per lane instead of waiting on each group)
+            u32 ent[2][4][K][W];
+            auto look = [&](int gq, u32 (&e)[4][K][W]) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int r = 4 * gq + rr;
 #pragma unroll
-                    for (int w = 0; w < W; ++w)
-                        row[rr * W + w] = 0;
-#pragma unroll
                     for (int c = 0; c < K; ++c) {
                         const u32 byte = (pv[u][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                        const u8 *e = tbl + tdep + c * TB + byte * E;
+                        const u8 *ep = tbl + c * TB + byte * E;
                         if constexpr (E == 8) {
-                            const uint2 t = *reinterpret_cast<const uint2 *>(e);
-                            row[rr * W] ^= t.x;
-                            row[rr * W + 1] ^= t.y;
+                            const uint2 t = *reinterpret_cast<const uint2 *>(ep);
+                            e[rr][c][0] = t.x;
+                            e[rr][c][W - 1] = t.y;
                         } else {
-                            row[rr * W] ^= *reinterpret_cast<const u32 *>(e);
+                            e[rr][c][0] = *reinterpret_cast<const u32 *>(ep);
                         }
                     }
                 }
+            };
+            look(0, ent[0]);
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                if (gq < 3)
+                    look(gq + 1, ent[(gq + 1) & 1]);
+                u32 row[4 * W];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        u32 x = ent[gq & 1][rr][0][w];
+#pragma unroll
+                        for (int c = 1; c < K; ++c)
+                            x ^= ent[gq & 1][rr][c][w];
+                        row[rr * W + w] = x;
+                    }
 #pragma unroll
                 for (int q = 0; q < K; ++q)
                     o[gq * K + q] = pack_dword<K, W>(row, q);
-                if constexpr (K * W > 8)
-                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(o[gq * K]));
             }
         }
         const u64 ubyte = u64(ru) * K;  // first output byte of the unit

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 a=$1; b=$2; shift 2
 for lib in "$a" "$b"; do
   echo "== $lib"
-  AB_NODEC=${AB_NODEC:-1} AB_ROUNDS=${AB_ROUNDS:-3} timeout -k 10 300 python -c "
+  AB_NODEC=${AB_NODEC-1} AB_ROUNDS=${AB_ROUNDS:-3} timeout -k 10 300 python -c "
 import sys; sys.path.insert(0, '.'); sys.path.insert(0, 'tools')
 import nkfs_amd._lib as l; l.LIB_PATH = '$lib'
 sys.argv = ['ab_tune'] + sys.argv[1:]
