@@ -26,16 +26,28 @@ def load(path):
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
     _lib.check(L.nkfs_gpu_init(0), path)
+    # AB_TUNE="enc_kernel=1,dec_kernel=2": the same struct nkfs_tune fields in every build
+    spec = os.environ.get("AB_TUNE", "")
+    if spec:
+        t = _lib.Tune()
+        L.nkfs_tune_get(C.byref(t))
+        for kv in spec.split(","):
+            key, val = kv.split("=")
+            setattr(t, key, int(val))
+        _lib.check(L.nkfs_tune_set(C.byref(t)), "nkfs_tune_set")
     return L
 
 
 def main():
     libs = [(p, load(p)) for p in sys.argv[1:] if p.endswith(".so")]
+    batch.gpu_init(0)  # the in-tree build synthesises the inputs
     for name in [a for a in sys.argv[1:] if not a.endswith(".so")]:
         S, B, n, k, _ = CONFIGS[name]
         ps = batch.part_size(B, k)
-        pitch = batch.part_pitch(B, k)
-        blocks = batch.synth(S, B)
+        # layout experiments: AB_PPAD / AB_BPAD bytes added to the part / block pitch
+        pitch = batch.part_pitch(B, k) + int(os.environ.get("AB_PPAD", "0"))
+        bpitch = B + int(os.environ.get("AB_BPAD", "0"))
+        blocks = batch.synth(S, B, pitch=bpitch)
         ids = torch.from_numpy(synth.batch_ids(S, n)).cuda()
         avail = torch.from_numpy(synth.batch_survivors(S, n, k)).cuda()
         parts = torch.empty((S * n, pitch), dtype=torch.uint8, device="cuda")
@@ -49,7 +61,7 @@ def main():
         res = {}
         for _ in range(5):
             for path, L in libs:
-                te = timeit(lambda: L.nkfs_nk8_encode(blocks.data_ptr(), blocks.stride(0), B, S, n, k, ids.data_ptr(),
+                te = timeit(lambda: L.nkfs_nk8_encode(blocks.data_ptr(), bpitch, B, S, n, k, ids.data_ptr(),
                                                       parts.data_ptr(), pitch, dig.data_ptr(), s), 10)
                 td = timeit(lambda: L.nkfs_nk8_decode(parts.data_ptr(), pitch, n, ids.data_ptr(), avail.data_ptr(),
                                                       k, k, B, out.data_ptr(), B, S, work.data_ptr(), st.data_ptr(),
