@@ -57,11 +57,14 @@ int nkfs_gpu_get_devices(int *devices, int max);
  * starts with the measured defaults; tools and tests replace
  * them with nkfs_tune_set to compare kernels in one process.  The launchers
  * read only this struct: no environment variable changes what runs. */
-enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC };
-enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC };
+/* NKFS_ENC_WIDE: part-group encoder (any n, k <= 16; the default beyond the
+ * fused kernels' n <= 8, k <= 8); NKFS_ENC_GENERIC: thread-per-row kernel */
+enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE };
+/* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16) */
+enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE };
 struct nkfs_tune {
-	int enc_kernel;       /* NKFS_ENC_*: encoder for n <= 8, k <= 8 */
-	int dec_kernel;       /* NKFS_DEC_*: decoder for k <= 8 */
+	int enc_kernel;       /* NKFS_ENC_*: encoder (WIDE / GENERIC also pin n <= 8 shapes) */
+	int dec_kernel;       /* NKFS_DEC_*: decoder (WIDE / GENERIC also pin k <= 8) */
 	int enc_waves_per_cu; /* resident waves per CU of the walk encoder (1..32) */
 	int dec_waves_per_cu; /* resident waves per CU of the slice decoder (1..32) */
 	int dec_units;        /* 1,024-row units per slice-decoder wave (1, 2 or 4) */

@@ -580,6 +580,9 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,
                                 int cus, hipStream_t st);
+extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st);
+extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
+                                hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                  void *work, int32_t *status, const void *gf, int units, int waves, hipStream_t st);
 
@@ -638,13 +641,21 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         return 0;
     hipStream_t st = (hipStream_t)stream;
     int rc = -ENOSYS;
-    if (g->n <= 8 && g->k <= 8 && nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC && !few_big_stripes(g)) {
+    const int kern = nkfs_g_tune.enc_kernel;
+    if (g->n <= 8 && g->k <= 8 && kern != NKFS_ENC_GENERIC && kern != NKFS_ENC_WIDE && !few_big_stripes(g)) {
         rc = with_size_order(g, st, [&](const nkfs_geom *go) { return fast_encode(go, ids, digests, st); });
         if (rc == -ENOSYS)
             rc = fast_encode(g, ids, digests, st);
     }
     if (rc != -ENOSYS)
         return rc;
+    // n > 8 (or a few big stripes): part groups of 8 for k <= 16, then the
+    // batched XXH64 of the parts
+    if (kern != NKFS_ENC_GENERIC) {
+        rc = nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
+        if (rc != -ENOSYS)
+            return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
+    }
     const u32 ps = max_part_size(g, g->block_size);
     dim3 grid(g->nstripes, row_blocks(ps));
     hipLaunchKernelGGL(k_encode_generic, grid, dim3(256), 0, st, *g, ids, (const GfTables *)gf);
@@ -676,7 +687,7 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     hipStream_t st = (hipStream_t)stream;
     const nkfs_tune &t = nkfs_g_tune;
     int rc = -ENOSYS;
-    if (g->k <= 8 && t.dec_kernel != NKFS_DEC_GENERIC) {
+    if (g->k <= 8 && t.dec_kernel != NKFS_DEC_GENERIC && t.dec_kernel != NKFS_DEC_WIDE) {
         // uniform batches without the integrity check: one-shot slice waves;
         // ragged batches and the verifying form: the wave-per-stripe decoder
         // default: one-shot slices for k >= 3 (C3/C4 decode +10-15 %); for
@@ -700,11 +711,18 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     rc = launch_ok();
     if (rc)
         return rc;
-    const u32 ps = part_size_of(g->block_size, g->k);
-    dim3 grid(g->nstripes, row_blocks(ps));
-    hipLaunchKernelGGL(k_decode_generic, grid, dim3(256), 0, st, *g, n_slots, (const u8 *)work,
-                       (const int32_t *)status, (const GfTables *)gf);
-    if ((rc = launch_ok()) || !expect)
+    // k <= 16: survivor tables of 16-byte products (nk8_wide.hip); beyond,
+    // or pinned: thread per row
+    rc = t.dec_kernel != NKFS_DEC_GENERIC ? nkfs_wide_decode(g, (const u8 *)work, status, nkfs_cu_count(), st)
+                                          : -ENOSYS;
+    if (rc == -ENOSYS) {
+        const u32 ps = part_size_of(g->block_size, g->k);
+        dim3 grid(g->nstripes, row_blocks(ps));
+        hipLaunchKernelGGL(k_decode_generic, grid, dim3(256), 0, st, *g, n_slots, (const u8 *)work,
+                           (const int32_t *)status, (const GfTables *)gf);
+        rc = launch_ok();
+    }
+    if (rc || !expect)
         return rc;
     hipLaunchKernelGGL(k_verify_generic, dim3(g->nstripes), dim3(64), 0, st, *g, n_slots, (const u8 *)work, status,
                        expect, badmask);

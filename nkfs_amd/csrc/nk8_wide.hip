@@ -1,0 +1,394 @@
+// nk8_wide.hip -- the shapes the fused kernels do not take: encode with
+// n > 8 parts (up to 255) and 2 <= k <= 16, or a handful of big stripes (one
+// nk8_split_block call); decode with 8 < k <= 16.
+//
+// Reference: crt/nk8.c:403-420 -- part_i[j] = XOR_m ids[i]^m * d[j*k + m],
+// d zero past block_size (:393-398); crt/nk8.c:552-582 -- block[j*k + m] =
+// XOR_c part_c[j] * W[c][m], W the inverse of the survivors' Vandermonde rows.
+//
+// Parts are taken eight at a time (a "part group"): for a stripe and group,
+// the packed tables T_m[x] = (ids_{8g}^m x, ..., ids_{8g+7}^m x), m = 1..k-1,
+// give one row's term for eight parts per ds_read_b64, exactly as in the
+// fused kernels; k-1 lookups + XORs per row and group.  A workgroup (4
+// waves) owns one (stripe, group, row slice): it builds the group's tables
+// once in LDS, then every lane encodes 16 rows per step (k 16-byte loads of
+// its contiguous 16k bytes; 16 bytes of each of the group's parts out,
+// one contiguous 1 KiB run per store instruction).  A stripe's groups read
+// the same block, so they are placed on the same XCD (MI355X hands
+// workgroup b to XCD b mod 8) and share its L2: the block comes from HBM
+// about once whatever the group count.  Big stripes are cut into row slices
+// so that a few stripes still fill the chip.  XXH64 of the parts runs
+// afterwards as the batched message hash (k_xxh64_fast), since one part's
+// chain is serial over all of its rows.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include "nk8_dev.h"
+
+using namespace nkfs;
+using namespace nkfs::dev;
+
+namespace {
+
+constexpr int WIDE_MAX_K = 16;
+constexpr u32 STEP_ROWS = 4 * 1024;  // rows a workgroup encodes per step
+
+template <int K>
+__global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids, u32 ngroups, u32 nslices,
+                                                     u32 slice_rows)
+{
+    constexpr int TB = 256 * 8;  // bytes per packed table
+    __shared__ __attribute__((aligned(16))) u8 tbl[(K - 1) * TB];
+
+    // block -> (stripe, group, slice); the groups and slices of stripe s all
+    // land on XCD s mod 8
+    const u32 b = blockIdx.x;
+    const u32 loc = b >> 3;
+    const u32 slice = loc % nslices;
+    const u32 grp = (loc / nslices) % ngroups;
+    const u32 s = (loc / nslices / ngroups) * 8 + (b & 7);
+    if (s >= g.nstripes)
+        return;  // the whole workgroup: no barrier is skipped by part of it
+    const Stripe v = stripe_at(g, s);
+    const u32 r_begin = slice * slice_rows;
+    if (r_begin >= v.ps)
+        return;
+    const u32 r_end = min(v.ps, r_begin + slice_rows);
+    const int n = g.n;
+    const int i0 = int(grp) * 8;
+    const int ne = min(8, n - i0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+
+    // tables of parts i0..i0+7 (coefficient 0 past n: those entries are 0
+    // and nothing is stored for them); wave w builds T_m for m-1 = w mod 4
+    u32 idw[2] = {0, 0};
+    for (int e = 0; e < ne; ++e)
+        idw[e >> 2] |= u32(ids[u64(s) * u64(n) + u64(i0 + e)]) << (8 * (e & 3));
+    u32 coef[2] = {idw[0], idw[1]};
+#pragma unroll
+    for (int m = 1; m < K; ++m) {
+        if ((m - 1) % 4 == wave) {
+            u32 basis[8][2];
+            make_basis<2>(basis, coef);
+            build_table<2, 64>(tbl + (m - 1) * TB, basis, lane);
+        }
+        coef[0] = gf_mul_packed(coef[0], idw[0]);
+        coef[1] = gf_mul_packed(coef[1], idw[1]);
+    }
+    __syncthreads();
+
+    const bool aligned =
+        ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
+    for (u32 r0 = r_begin + u32(wave) * 1024u + 16u * u32(lane); r0 < r_end; r0 += STEP_ROWS) {
+        // 16 rows = 16k bytes of the block (zero past B)
+        u32 d[4 * K];
+        const u64 off = u64(r0) * K;
+        if (aligned && off + 16 * K <= v.B) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const uint4 t = src[q];
+                d[4 * q] = t.x;
+                d[4 * q + 1] = t.y;
+                d[4 * q + 2] = t.z;
+                d[4 * q + 3] = t.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4 * K; ++q) {
+                u32 x = 0;
+                for (int c = 0; c < 4; ++c) {
+                    const u64 p = off + 4 * q + c;
+                    if (p < v.B)
+                        x |= u32(v.blk[p]) << (8 * c);
+                }
+                d[q] = x;
+            }
+        }
+        // four groups of 4 rows: lookups + XOR, then 4 rows x 8 bytes are
+        // transposed into 4 bytes of each of the 8 parts
+        u32 out[8][4];
+        u32 tdep = 0;  // 0 at run time; orders each group's lookups after the previous group
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u32 row[4][2];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int p0 = (4 * q + rr) * K;
+                const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
+                row[rr][0] = rep;
+                row[rr][1] = rep;
+#pragma unroll
+                for (int m = 1; m < K; ++m) {
+                    const int p = p0 + m;
+                    const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                    const uint2 t = *reinterpret_cast<const uint2 *>(tbl + tdep + (m - 1) * TB + byte * 8);
+                    row[rr][0] ^= t.x;
+                    row[rr][1] ^= t.y;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < 2; ++w)
+                transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[4 * w][q], out[4 * w + 1][q],
+                           out[4 * w + 2][q], out[4 * w + 3][q]);
+            // without this the compiler hoists all 16 rows' lookups up front
+            // and holds 32 (k-1) results in VGPRs
+            if constexpr (K > 4)
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(out[0][q]));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i < ne) {
+                u8 *dst = v.parts + u64(i0 + i) * v.pitch + r0;
+                if (aligned && r0 + 16 <= v.ps) {
+                    store16(dst, out[i][0], out[i][1], out[i][2], out[i][3], false);
+                } else {
+                    for (int c = 0; c < 16 && r0 + c < v.ps; ++c)
+                        dst[c] = u8(out[i][c >> 2] >> (8 * (c & 3)));
+                }
+            }
+        }
+    }
+}
+
+
+// Packed 16-byte table T[x] = XOR_{bit b of x} basis[b] for one 64-lane wave
+// (lane li owns x = li + 64 j, Gray-code order: one XOR per entry and word).
+__device__ inline void build_table16(u8 *t, const u32 (&basis)[8][4], int li)
+{
+    u32 hv[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        u32 e = 0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b)
+            e ^= basis[b][w] & (0u - ((u32(li) >> b) & 1u));
+        hv[w] = e;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j) {
+            const int bit = __builtin_ctz(j);
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                hv[w] ^= basis[6 + bit][w];
+        }
+        const int x = li + 64 * (j ^ (j >> 1));
+        *reinterpret_cast<uint4 *>(t + x * 16) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+    }
+}
+
+// Decode, 2 <= k <= 16: one workgroup (4 waves) per (stripe, row slice).
+// Survivor c's table U_c[x] = (W[c][0] x, ..., W[c][15] x) packs the
+// products for all k output bytes of a row, so a row costs k ds_read_b128 +
+// XORs.  A lane rebuilds 16 rows per step from 16 bytes of each of the k
+// survivor parts (k 16-byte loads, one contiguous 1 KiB run per instruction)
+// and writes the 16 rows' 16k contiguous block bytes.  The selection and W
+// come from k_decode_prep (work: k slot numbers, then W row-major).
+template <int K>
+__global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work, const int32_t *status,
+                                                     u32 nslices, u32 slice_rows)
+{
+    constexpr int TB = 256 * 16;  // bytes per packed table
+    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
+    const u32 b = blockIdx.x;
+    const u32 slice = (b >> 3) % nslices;
+    const u32 s = (b >> 3) / nslices * 8 + (b & 7);
+    if (s >= g.nstripes || (status && status[s]))
+        return;
+    const Stripe v = stripe_at(g, s);  // g.blocks = the output, g.n = slots per stripe
+    const u32 r_begin = slice * slice_rows;
+    if (r_begin >= v.ps)
+        return;
+    const u32 r_end = min(v.ps, r_begin + slice_rows);
+    const u8 *wk = work + u64(s) * u64(K + K * K);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        if (c % 4 == wave) {
+            u32 row[4] = {0, 0, 0, 0};
+            for (int m = 0; m < K; ++m)
+                row[m >> 2] |= u32(wk[K + c * K + m]) << (8 * (m & 3));
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            build_table16(tbl + c * TB, basis, lane);
+        }
+    }
+    const u8 *src[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+        src[c] = v.parts + u64(wk[c]) * v.pitch;
+    __syncthreads();
+
+    u8 *out = const_cast<u8 *>(v.blk);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
+    for (u32 r0 = r_begin + u32(wave) * 1024u + 16u * u32(lane); r0 < r_end; r0 += STEP_ROWS) {
+        // 16 bytes of each survivor part (zero past the part)
+        u32 p[K][4];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            if (aligned && r0 + 16 <= v.ps) {
+                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);
+                p[c][0] = t.x;
+                p[c][1] = t.y;
+                p[c][2] = t.z;
+                p[c][3] = t.w;
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    u32 x = 0;
+                    for (int e = 0; e < 4; ++e)
+                        if (r0 + 4 * w + e < v.ps)
+                            x |= u32(src[c][r0 + 4 * w + e]) << (8 * e);
+                    p[c][w] = x;
+                }
+            }
+        }
+        // four groups of 4 rows; each group's 4K output bytes are K dwords
+        u32 o[4 * K];
+        u32 tdep = 0;  // 0 at run time; orders each group's lookups after the previous group
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u32 row[4][4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int j = 4 * q + rr;  // row within the lane's 16
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    row[rr][w] = 0;
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    const u32 x = (p[c][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const uint4 t = *reinterpret_cast<const uint4 *>(tbl + tdep + c * TB + x * 16);
+                    row[rr][0] ^= t.x;
+                    row[rr][1] ^= t.y;
+                    row[rr][2] ^= t.z;
+                    row[rr][3] ^= t.w;
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < K; ++d)
+                o[q * K + d] = pack_dword<K, 4>(&row[0][0], d);
+            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(o[q * K]));
+        }
+        // rows r0..r0+15 = block bytes [r0 K, r0 K + 16 K): K 16-byte stores
+        const u64 off = u64(r0) * K;
+        if (aligned && off + 16 * K <= v.B) {
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                store16(out + off + 16 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], false);
+        } else {
+            for (int i = 0; i < 16 * K && off + i < v.B; ++i)
+                out[off + i] = u8(o[i >> 2] >> (8 * (i & 3)));
+        }
+    }
+}
+
+// row slices so that the grid has about `min_wgs` workgroups (never a slice
+// below one step): returns slices, sets *rows
+u64 slices_for(u64 base, u32 ps_max, int cus, u64 *rows)
+{
+    const u64 steps = (u64(ps_max) + STEP_ROWS - 1) / STEP_ROWS;  // >= 1
+    const u64 min_wgs = u64(cus > 0 ? cus : 256) * 8;
+    u64 ns = (min_wgs + base - 1) / base;
+    ns = ns > steps ? steps : ns < 1 ? 1 : ns;
+    *rows = (steps + ns - 1) / ns * STEP_ROWS;
+    ns = (u64(ps_max) + *rows - 1) / *rows;
+    return ns < 1 ? 1 : ns;
+}
+
+}  // namespace
+
+// Encode (no hash) a uniform or ragged batch with 2 <= k <= 16, any n <= 255.
+// Workgroups: ceil(nstripes / 8) * 8 stripes x ceil(n / 8) groups x row
+// slices, the slices chosen so that the grid has at least `min_wgs`
+// workgroups when the stripes are big enough to be cut.  -ENOSYS for k > 16.
+extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st)
+{
+    const int k = g->k;
+    if (k < 2 || k > WIDE_MAX_K || g->n < k || g->n > 255)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 ngroups = u64(g->n + 7) / 8;
+    const u64 base = (u64(g->nstripes) + 7) / 8 * 8 * ngroups;
+    u64 slice_rows = 0;
+    const u64 nslices = slices_for(base, ps_max, cus, &slice_rows);
+    const u64 grid = base * nslices;
+    if (grid > 0x7FFFFFFFull || slice_rows > 0xFFFFFFFFull)
+        return -EINVAL;
+    const dim3 gd = dim3(u32(grid)), bd = dim3(256);
+    switch (k) {
+#define NKFS_K(KK)                                                                                       \
+    case KK:                                                                                             \
+        hipLaunchKernelGGL(k_encode_wide<KK>, gd, bd, 0, st, *g, ids, u32(ngroups), u32(nslices),        \
+                           u32(slice_rows));                                                             \
+        break;
+        NKFS_K(2)
+        NKFS_K(3)
+        NKFS_K(4)
+        NKFS_K(5)
+        NKFS_K(6)
+        NKFS_K(7)
+        NKFS_K(8)
+        NKFS_K(9)
+        NKFS_K(10)
+        NKFS_K(11)
+        NKFS_K(12)
+        NKFS_K(13)
+        NKFS_K(14)
+        NKFS_K(15)
+        NKFS_K(16)
+#undef NKFS_K
+    default:
+        return -ENOSYS;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// Decode a uniform or ragged batch with 2 <= k <= 16 from the plan
+// k_decode_prep left in `work` (stripes with status != 0 are skipped).
+extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
+                                hipStream_t st)
+{
+    const int k = g->k;
+    if (k < 2 || k > WIDE_MAX_K)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 base = (u64(g->nstripes) + 7) / 8 * 8;
+    u64 slice_rows = 0;
+    const u64 nslices = slices_for(base, ps_max, cus, &slice_rows);
+    const u64 grid = base * nslices;
+    if (grid > 0x7FFFFFFFull || slice_rows > 0xFFFFFFFFull)
+        return -EINVAL;
+    const dim3 gd = dim3(u32(grid)), bd = dim3(256);
+    switch (k) {
+#define NKFS_K(KK)                                                                                       \
+    case KK:                                                                                             \
+        hipLaunchKernelGGL(k_decode_wide<KK>, gd, bd, 0, st, *g, work, status, u32(nslices), u32(slice_rows)); \
+        break;
+        NKFS_K(2)
+        NKFS_K(3)
+        NKFS_K(4)
+        NKFS_K(5)
+        NKFS_K(6)
+        NKFS_K(7)
+        NKFS_K(8)
+        NKFS_K(9)
+        NKFS_K(10)
+        NKFS_K(11)
+        NKFS_K(12)
+        NKFS_K(13)
+        NKFS_K(14)
+        NKFS_K(15)
+        NKFS_K(16)
+#undef NKFS_K
+    default:
+        return -ENOSYS;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

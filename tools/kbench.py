@@ -4,8 +4,8 @@
 
 For each config: encode+hash, encode alone (d_digests = NULL), decode, and
 the batched XXH64 of the parts, each averaged over per-launch HIP event
-pairs on the launch stream.  Env knobs the library reads (NKFS_ENC_PREFETCH,
-NKFS_FORCE_GENERIC) can be varied per process."""
+pairs on the launch stream.  A config is a bench.py name or S:B:n:k; kernels
+are pinned through struct nkfs_tune (KB_TUNE="enc_kernel=4,dec_kernel=3")."""
 import os
 import sys
 
@@ -53,6 +53,13 @@ def clusters(count=16384, ch=65536, page=4096):
 def main():
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(0))
+    spec = os.environ.get("KB_TUNE", "")
+    if spec:
+        t = _lib.get_tune()
+        for kv in spec.split(","):
+            key, val = kv.split("=")
+            setattr(t, key, int(val))
+        _lib.check(L.nkfs_tune_set(_lib.C.byref(t)), "nkfs_tune_set")
     for name in sys.argv[1:] or ["c2", "c4"]:
         if name == "clu":
             clusters()
@@ -65,7 +72,10 @@ def main():
                 print(f"clu {count:6d} x {ch:6d} pitch {pitch:6d} {t*1e6:9.1f} us {count*ch/t/1e9:7.1f} GB/s")
                 del d
             continue
-        S, B, n, k, _ = CONFIGS[name]
+        if ":" in name:  # S:B:n:k
+            S, B, n, k = (int(x) for x in name.split(":"))
+        else:
+            S, B, n, k, _ = CONFIGS[name]
         ps = batch.part_size(B, k)
         blocks = batch.synth(S, B)
         ids = torch.from_numpy(synth.batch_ids(S, n)).cuda()
