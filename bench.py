@@ -46,6 +46,10 @@ CONFIGS = {
     "c3": (8192, 1048576, 8, 5, "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 8192 x 1 MiB stripes (8 GiB) "
                                 "per GPU"),
     "c4": (16384, 262144, 8, 5, "C4: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 16384 x 256 KiB stripes per GPU"),
+    # beyond the BASELINE configs: n > 8, k > 8 (SURVEY.md §8 a5/a8 for general n, k) on the
+    # part-group encoder and survivor-table decoder (nk8_wide.hip); XXH64 is a second pass over the parts
+    "w1": (2048, 1048576, 16, 12, "W1: N=16,K=12 encode(+XXH64/part)+decode(4 erased), 2048 x 1 MiB stripes per "
+                                  "GPU (general n,k path; not a BASELINE config)"),
     # ragged: block size of every stripe drawn from C5_SIZES (synth.mixed_sizes)
     "c5": (11520, None, 8, 5, "C5: N=8,K=5 encode(+XXH64/part)+decode(3 erased) of a ragged batch, stripe sizes "
                               "uniform over {4 KiB, 64 KiB, 1 MiB}, ~4 GiB per GPU, byte-balanced over the GPUs"),
@@ -433,7 +437,7 @@ def main():
     top = run(head, args.steps)
     subs = {}
     if args.config == "all":
-        for name in ("c2", "c4", "c5"):
+        for name in ("c2", "c4", "c5", "w1"):
             subs[name] = run(name, None)
     result = {
         "metric": METRIC, "value": top.pop("value"), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,

@@ -41,9 +41,11 @@ for k, cs in sorted(out.items(), key=lambda kv: -sum(kv[1].values())):
     print(f"{k[:70]:70s} FETCH {f/1e6:10.1f} MB (x2 {2*f/1e6:10.1f})  WRITE {w/1e6:10.1f} MB")
     # one encode (decode) call may be several kernels (a ragged batch split
     # by part size: k_encode_ws + k_encode_fast, each launched once per call),
-    # so the per-call traffic is the sum of their per-dispatch means
+    # so the per-call traffic is the sum of their per-dispatch means; the
+    # batched XXH64 of the parts (k_xxh64_*) belongs to the encode call of the
+    # general n, k path (nk8_wide.hip encodes, then hashes the parts)
     for kind in ("encode", "decode"):
-        if f"k_{kind}" in k:
+        if f"k_{kind}" in k or (kind == "encode" and "k_xxh64" in k):
             rec[f"{kind}_kernel"] = (rec[f"{kind}_kernel"] + " + " + k) if f"{kind}_kernel" in rec else k
             for key, val in ((f"{kind}_bytes_per_launch", 2 * f + w), (f"{kind}_fetch_size_x2", 2 * f),
                              (f"{kind}_write_size", w)):
