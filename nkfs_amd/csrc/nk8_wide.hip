@@ -10,13 +10,13 @@
 // the packed tables T_m[x] = (ids_{8g}^m x, ..., ids_{8g+7}^m x), m = 1..k-1,
 // give one row's term for eight parts per ds_read_b64, exactly as in the
 // fused kernels; k-1 lookups + XORs per row and group.  A workgroup (4
-// waves) owns one (stripe, group, row slice): it builds the group's tables
-// once in LDS, then every lane encodes 16 rows per step (k 16-byte loads of
-// its contiguous 16k bytes; 16 bytes of each of the group's parts out,
-// one contiguous 1 KiB run per store instruction).  A stripe's groups read
-// the same block, so they are placed on the same XCD (MI355X hands
-// workgroup b to XCD b mod 8) and share its L2: the block comes from HBM
-// about once whatever the group count.  Big stripes are cut into row slices
+// waves) owns one (stripe, two groups, row slice): it builds the groups'
+// tables once in LDS, then every lane encodes 16 rows per step (k 16-byte
+// loads of its contiguous 16k bytes, read once for 16 parts; 16 bytes of
+// each part out, one contiguous 1 KiB run per store instruction).  With
+// more than 16 parts the group pairs of a stripe read the same block, so
+// they are placed on the same XCD (MI355X hands workgroup b to XCD b mod 8)
+// and share its L2.  Big stripes are cut into row slices
 // so that a few stripes still fill the chip.  XXH64 of the parts runs
 // afterwards as the batched message hash (k_xxh64_fast), since one part's
 // chain is serial over all of its rows.
@@ -34,19 +34,19 @@ namespace {
 constexpr int WIDE_MAX_K = 16;
 constexpr u32 STEP_ROWS = 4 * 1024;  // rows a workgroup encodes per step
 
-template <int K>
+template <int K, int NG>
 __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids, u32 ngroups, u32 nslices,
                                                      u32 slice_rows)
 {
     constexpr int TB = 256 * 8;  // bytes per packed table
-    __shared__ __attribute__((aligned(16))) u8 tbl[(K - 1) * TB];
+    __shared__ __attribute__((aligned(16))) u8 tbl[NG][(K - 1) * TB];
 
-    // block -> (stripe, group, slice); the groups and slices of stripe s all
-    // land on XCD s mod 8
+    // block -> (stripe, NG consecutive groups, slice); the group sets and
+    // slices of stripe s all land on XCD s mod 8
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
     const u32 slice = loc % nslices;
-    const u32 grp = (loc / nslices) % ngroups;
+    const u32 gset = (loc / nslices) % ngroups;
     const u32 s = (loc / nslices / ngroups) * 8 + (b & 7);
     if (s >= g.nstripes)
         return;  // the whole workgroup: no barrier is skipped by part of it
@@ -56,32 +56,41 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
         return;
     const u32 r_end = min(v.ps, r_begin + slice_rows);
     const int n = g.n;
-    const int i0 = int(grp) * 8;
-    const int ne = min(8, n - i0);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-
-    // tables of parts i0..i0+7 (coefficient 0 past n: those entries are 0
-    // and nothing is stored for them); wave w builds T_m for m-1 = w mod 4
-    u32 idw[2] = {0, 0};
-    for (int e = 0; e < ne; ++e)
-        idw[e >> 2] |= u32(ids[u64(s) * u64(n) + u64(i0 + e)]) << (8 * (e & 3));
-    u32 coef[2] = {idw[0], idw[1]};
+    int i0[NG], ne[NG];
 #pragma unroll
-    for (int m = 1; m < K; ++m) {
-        if ((m - 1) % 4 == wave) {
-            u32 basis[8][2];
-            make_basis<2>(basis, coef);
-            build_table<2, 64>(tbl + (m - 1) * TB, basis, lane);
+    for (int h = 0; h < NG; ++h) {
+        i0[h] = (int(gset) * NG + h) * 8;
+        ne[h] = max(0, min(8, n - i0[h]));
+    }
+
+    // tables of parts i0..i0+7 of each group (coefficient 0 past n: those
+    // entries are 0 and nothing is stored for them); wave w builds T_m for
+    // m-1 = w mod 4
+#pragma unroll
+    for (int h = 0; h < NG; ++h) {
+        u32 idw[2] = {0, 0};
+        for (int e = 0; e < ne[h]; ++e)
+            idw[e >> 2] |= u32(ids[u64(s) * u64(n) + u64(i0[h] + e)]) << (8 * (e & 3));
+        u32 coef[2] = {idw[0], idw[1]};
+#pragma unroll
+        for (int m = 1; m < K; ++m) {
+            if ((m - 1) % 4 == wave) {
+                u32 basis[8][2];
+                make_basis<2>(basis, coef);
+                build_table<2, 64>(tbl[h] + (m - 1) * TB, basis, lane);
+            }
+            coef[0] = gf_mul_packed(coef[0], idw[0]);
+            coef[1] = gf_mul_packed(coef[1], idw[1]);
         }
-        coef[0] = gf_mul_packed(coef[0], idw[0]);
-        coef[1] = gf_mul_packed(coef[1], idw[1]);
     }
     __syncthreads();
 
     const bool aligned =
         ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
     for (u32 r0 = r_begin + u32(wave) * 1024u + 16u * u32(lane); r0 < r_end; r0 += STEP_ROWS) {
-        // 16 rows = 16k bytes of the block (zero past B)
+        // 16 rows = 16k bytes of the block (zero past B), read once for all
+        // NG groups
         u32 d[4 * K];
         const u64 off = u64(r0) * K;
         if (aligned && off + 16 * K <= v.B) {
@@ -106,52 +115,56 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
                 d[q] = x;
             }
         }
-        // four groups of 4 rows: lookups + XOR, then 4 rows x 8 bytes are
-        // transposed into 4 bytes of each of the 8 parts
-        u32 out[8][4];
-        u32 tdep = 0;  // 0 at run time; orders each group's lookups after the previous group
+        u32 tdep = 0;  // 0 at run time; orders each row group's lookups after the previous one
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            u32 row[4][2];
+        for (int h = 0; h < NG; ++h) {
+            // four groups of 4 rows: lookups + XOR, then 4 rows x 8 bytes
+            // are transposed into 4 bytes of each of the 8 parts
+            u32 out[8][4];
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int p0 = (4 * q + rr) * K;
-                const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
-                row[rr][0] = rep;
-                row[rr][1] = rep;
+            for (int q = 0; q < 4; ++q) {
+                u32 row[4][2];
 #pragma unroll
-                for (int m = 1; m < K; ++m) {
-                    const int p = p0 + m;
-                    const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
-                    const uint2 t = *reinterpret_cast<const uint2 *>(tbl + tdep + (m - 1) * TB + byte * 8);
-                    row[rr][0] ^= t.x;
-                    row[rr][1] ^= t.y;
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int p0 = (4 * q + rr) * K;
+                    const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
+                    row[rr][0] = rep;
+                    row[rr][1] = rep;
+#pragma unroll
+                    for (int m = 1; m < K; ++m) {
+                        const int p = p0 + m;
+                        // (| tdep: no common subexpression across groups,
+                        // which would keep 16 (k-1) extracted bytes live)
+                        const u32 byte = ((d[p >> 2] | tdep) >> (8 * (p & 3))) & 0xFFu;
+                        const uint2 t = *reinterpret_cast<const uint2 *>(tbl[h] + tdep + (m - 1) * TB + byte * 8);
+                        row[rr][0] ^= t.x;
+                        row[rr][1] ^= t.y;
+                    }
                 }
+#pragma unroll
+                for (int w = 0; w < 2; ++w)
+                    transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[4 * w][q], out[4 * w + 1][q],
+                               out[4 * w + 2][q], out[4 * w + 3][q]);
+                // without this the compiler hoists all 16 rows' lookups up
+                // front and holds 32 (k-1) results in VGPRs
+                if constexpr (K > 4)
+                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(out[0][q]));
             }
 #pragma unroll
-            for (int w = 0; w < 2; ++w)
-                transpose4(row[0][w], row[1][w], row[2][w], row[3][w], out[4 * w][q], out[4 * w + 1][q],
-                           out[4 * w + 2][q], out[4 * w + 3][q]);
-            // without this the compiler hoists all 16 rows' lookups up front
-            // and holds 32 (k-1) results in VGPRs
-            if constexpr (K > 4)
-                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(out[0][q]));
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i < ne) {
-                u8 *dst = v.parts + u64(i0 + i) * v.pitch + r0;
-                if (aligned && r0 + 16 <= v.ps) {
-                    store16(dst, out[i][0], out[i][1], out[i][2], out[i][3], false);
-                } else {
-                    for (int c = 0; c < 16 && r0 + c < v.ps; ++c)
-                        dst[c] = u8(out[i][c >> 2] >> (8 * (c & 3)));
+            for (int i = 0; i < 8; ++i) {
+                if (i < ne[h]) {
+                    u8 *dst = v.parts + u64(i0[h] + i) * v.pitch + r0;
+                    if (aligned && r0 + 16 <= v.ps) {
+                        store16(dst, out[i][0], out[i][1], out[i][2], out[i][3], false);
+                    } else {
+                        for (int c = 0; c < 16 && r0 + c < v.ps; ++c)
+                            dst[c] = u8(out[i][c >> 2] >> (8 * (c & 3)));
+                    }
                 }
             }
         }
     }
 }
-
 
 // Packed 16-byte table T[x] = XOR_{bit b of x} basis[b] for one 64-lane wave
 // (lane li owns x = li + 64 j, Gray-code order: one XOR per entry and word).
@@ -182,16 +195,24 @@ __device__ inline void build_table16(u8 *t, const u32 (&basis)[8][4], int li)
 // Decode, 2 <= k <= 16: one workgroup (4 waves) per (stripe, row slice).
 // Survivor c's table U_c[x] = (W[c][0] x, ..., W[c][15] x) packs the
 // products for all k output bytes of a row, so a row costs k ds_read_b128 +
-// XORs.  A lane rebuilds 16 rows per step from 16 bytes of each of the k
-// survivor parts (k 16-byte loads, one contiguous 1 KiB run per instruction)
-// and writes the 16 rows' 16k contiguous block bytes.  The selection and W
-// come from k_decode_prep (work: k slot numbers, then W row-major).
+// XORs.  A wave rebuilds 1,024 rows per step in four runs of 256 rows: lane
+// l takes rows 4l..4l+3 of a run (one dword of each survivor part; the
+// step's 4k loads are issued up front), packs them to 4k block bytes, and
+// the run's 256k contiguous bytes go through a per-wave LDS stage so that
+// every store instruction writes one contiguous 1 KiB run (direct stores
+// from the lanes would stride 4k bytes apart: PMC showed 2x the write
+// traffic for the 16k-byte stride of a 16-rows-per-lane form).  The
+// selection and W come from k_decode_prep (work: k slot numbers, then W
+// row-major).
 template <int K>
 __global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work, const int32_t *status,
                                                      u32 nslices, u32 slice_rows)
 {
-    constexpr int TB = 256 * 16;  // bytes per packed table
+    constexpr int TB = 256 * 16;   // bytes per packed table
+    constexpr int SB = 256 * K;    // stage bytes per wave: one run of 256 rows
+    constexpr int NST = (SB + 1023) / 1024;  // 1 KiB store instructions per run
     __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
+    __shared__ __attribute__((aligned(16))) u8 stage[4][SB];
     const u32 b = blockIdx.x;
     const u32 slice = (b >> 3) % nslices;
     const u32 s = (b >> 3) / nslices * 8 + (b & 7);
@@ -222,44 +243,42 @@ __global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work
     __syncthreads();
 
     u8 *out = const_cast<u8 *>(v.blk);
-    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
-    for (u32 r0 = r_begin + u32(wave) * 1024u + 16u * u32(lane); r0 < r_end; r0 += STEP_ROWS) {
-        // 16 bytes of each survivor part (zero past the part)
-        u32 p[K][4];
+    u8 *stg = stage[wave];
+    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
+    const bool oal = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    // wave-uniform loop: a middle slice holds whole steps (slice_rows is a
+    // multiple of 4,096), so rows past r_end exist only past ps, whose bytes
+    // lie past B and are never stored
+    for (u32 rw = r_begin + u32(wave) * 1024u; rw < r_end; rw += STEP_ROWS) {
+        u32 p[4][K];
 #pragma unroll
-        for (int c = 0; c < K; ++c) {
-            if (aligned && r0 + 16 <= v.ps) {
-                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);
-                p[c][0] = t.x;
-                p[c][1] = t.y;
-                p[c][2] = t.z;
-                p[c][3] = t.w;
-            } else {
+        for (int q = 0; q < 4; ++q) {
+            const u32 r0 = rw + 256u * q + 4u * lane;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
+            for (int c = 0; c < K; ++c) {
+                if (pal && r0 + 4 <= v.ps) {
+                    p[q][c] = *reinterpret_cast<const u32 *>(src[c] + r0);
+                } else {
                     u32 x = 0;
                     for (int e = 0; e < 4; ++e)
-                        if (r0 + 4 * w + e < v.ps)
-                            x |= u32(src[c][r0 + 4 * w + e]) << (8 * e);
-                    p[c][w] = x;
+                        if (r0 + e < v.ps)
+                            x |= u32(src[c][r0 + e]) << (8 * e);
+                    p[q][c] = x;
                 }
             }
         }
-        // four groups of 4 rows; each group's 4K output bytes are K dwords
-        u32 o[4 * K];
-        u32 tdep = 0;  // 0 at run time; orders each group's lookups after the previous group
+        u32 tdep = 0;  // 0 at run time; orders each run's lookups after the previous run
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             u32 row[4][4];
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int j = 4 * q + rr;  // row within the lane's 16
 #pragma unroll
                 for (int w = 0; w < 4; ++w)
                     row[rr][w] = 0;
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    const u32 x = (p[c][j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const u32 x = (p[q][c] >> (8 * rr)) & 0xFFu;
                     const uint4 t = *reinterpret_cast<const uint4 *>(tbl + tdep + c * TB + x * 16);
                     row[rr][0] ^= t.x;
                     row[rr][1] ^= t.y;
@@ -267,20 +286,29 @@ __global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work
                     row[rr][3] ^= t.w;
                 }
             }
+            // rows rw + 256q + 4l .. +3 = run bytes [4K l, 4K l + 4K)
 #pragma unroll
             for (int d = 0; d < K; ++d)
-                o[q * K + d] = pack_dword<K, 4>(&row[0][0], d);
-            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(o[q * K]));
-        }
-        // rows r0..r0+15 = block bytes [r0 K, r0 K + 16 K): K 16-byte stores
-        const u64 off = u64(r0) * K;
-        if (aligned && off + 16 * K <= v.B) {
+                *reinterpret_cast<u32 *>(stg + 4 * K * lane + 4 * d) = pack_dword<K, 4>(&row[0][0], d);
+            __builtin_amdgcn_wave_barrier();
+            const u64 base = u64(rw + 256u * q) * K;
 #pragma unroll
-            for (int q = 0; q < K; ++q)
-                store16(out + off + 16 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], false);
-        } else {
-            for (int i = 0; i < 16 * K && off + i < v.B; ++i)
-                out[off + i] = u8(o[i >> 2] >> (8 * (i & 3)));
+            for (int j = 0; j < NST; ++j) {
+                const u32 bo = 1024u * j + 16u * lane;
+                if (bo < u32(SB)) {
+                    const uint4 t = *reinterpret_cast<const uint4 *>(stg + bo);
+                    const u64 off = base + bo;
+                    if (oal && off + 16 <= v.B) {
+                        store16(out + off, t.x, t.y, t.z, t.w, false);
+                    } else if (off < v.B) {
+                        const u32 tw[4] = {t.x, t.y, t.z, t.w};
+                        for (int e = 0; e < 16 && off + e < v.B; ++e)
+                            out[off + e] = u8(tw[e >> 2] >> (8 * (e & 3)));
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(row[0][0]));
         }
     }
 }
@@ -301,7 +329,7 @@ u64 slices_for(u64 base, u32 ps_max, int cus, u64 *rows)
 }  // namespace
 
 // Encode (no hash) a uniform or ragged batch with 2 <= k <= 16, any n <= 255.
-// Workgroups: ceil(nstripes / 8) * 8 stripes x ceil(n / 8) groups x row
+// Workgroups: ceil(nstripes / 8) * 8 stripes x ceil(n / 16) group pairs x row
 // slices, the slices chosen so that the grid has at least `min_wgs`
 // workgroups when the stripes are big enough to be cut.  -ENOSYS for k > 16.
 extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st)
@@ -312,7 +340,12 @@ extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus,
     if (!g->nstripes)
         return 0;
     const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
-    const u64 ngroups = u64(g->n + 7) / 8;
+    // part groups of 8; a workgroup takes two groups (one read of the block
+    // for 16 parts) when n > 8 and the pair's tables and registers still
+    // leave 3 waves per SIMD (k <= 14; profiles/r02/wide_kbench.txt: N16K12
+    // encode 4.61 -> 4.78 TB/s, N20K16 at 2 waves per SIMD 3.57 -> 3.11)
+    const int NG = g->n > 8 && k <= 14 ? 2 : 1;
+    const u64 ngroups = (u64(g->n + 7) / 8 + NG - 1) / NG;
     const u64 base = (u64(g->nstripes) + 7) / 8 * 8 * ngroups;
     u64 slice_rows = 0;
     const u64 nslices = slices_for(base, ps_max, cus, &slice_rows);
@@ -323,8 +356,12 @@ extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus,
     switch (k) {
 #define NKFS_K(KK)                                                                                       \
     case KK:                                                                                             \
-        hipLaunchKernelGGL(k_encode_wide<KK>, gd, bd, 0, st, *g, ids, u32(ngroups), u32(nslices),        \
-                           u32(slice_rows));                                                             \
+        if (NG == 2)                                                                                     \
+            hipLaunchKernelGGL((k_encode_wide<KK, 2>), gd, bd, 0, st, *g, ids, u32(ngroups), u32(nslices), \
+                               u32(slice_rows));                                                         \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_encode_wide<KK, 1>), gd, bd, 0, st, *g, ids, u32(ngroups), u32(nslices), \
+                               u32(slice_rows));                                                         \
         break;
         NKFS_K(2)
         NKFS_K(3)
