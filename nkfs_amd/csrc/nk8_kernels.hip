@@ -584,7 +584,8 @@ extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus,
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
-                                 void *work, int32_t *status, const void *gf, int units, int waves, hipStream_t st);
+                                 void *work, int32_t *status, const void *gf, int units, int waves, int cus,
+                                 hipStream_t st);
 
 // Fast-path encoder choice (n <= 8, k <= 8), struct nkfs_tune.enc_kernel:
 // AUTO = the walk encoder for ragged batches (one wave per stripe in size
@@ -694,9 +695,16 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // k = 2 a 4 KiB stripe is one wave either way and the wave decoder's
         // in-wave inverse saves the plan launch
         const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel : g->k >= 3 ? NKFS_DEC_SLICE : NKFS_DEC_WAVE;
-        if (kern == NKFS_DEC_SLICE && !expect && !g->block_sizes)
-            rc = nkfs_slice_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_units, t.dec_waves_per_cu,
-                                   st);
+        if (kern == NKFS_DEC_SLICE && !expect) {
+            // ragged: in size order (largest first), so the grid's tail is short slices
+            auto slice = [&](const nkfs_geom *go) {
+                return nkfs_slice_decode(go, n_slots, ids, avail, navail, work, status, gf, t.dec_units,
+                                         t.dec_waves_per_cu, nkfs_cu_count(), st);
+            };
+            rc = with_size_order(g, st, slice);
+            if (rc == -ENOSYS)
+                rc = slice(g);
+        }
         if (rc == -ENOSYS)
             rc = with_size_order(g, st, [&](const nkfs_geom *go) {
                 return nkfs_fast_decode(go, n_slots, ids, avail, navail, status, gf, st, expect, badmask);

@@ -570,8 +570,13 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
 // XPOSE: output rows go through LDS so every store instruction writes one
 // contiguous 1 KiB run (lane l owns 16 rows = 16K contiguous bytes; stored
 // directly that is a 16K-byte lane stride).
-template <int K, int E, int U, bool XPOSE>
-__global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, const u8 *plan, u32 slices)
+// RAGGED: a persistent grid walks the (stripe, slice) list of a ragged
+// batch -- smap[w] = (processing position << 32) | slice of slice w (g.order
+// applied; k_slice_scan + k_slice_map), *stotal = all slices -- and each
+// slice is one pass of the same one-shot body.
+template <int K, int E, int U, bool XPOSE, bool RAGGED>
+__global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, const u8 *plan, u32 slices,
+                                                     const u64 *smap, const u32 *stotal)
 {
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
@@ -581,24 +586,43 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
     __shared__ __attribute__((aligned(16))) u8 obuf[XPOSE ? 64 * LS : 16];
 
     const int li = threadIdx.x;
-    const u32 s = blockIdx.x / slices, slice = blockIdx.x % slices;
-    if (s >= g.nstripes)
-        return;
+    const u32 total = RAGGED ? *stotal : 0u;
+    for (u32 w = blockIdx.x;; w += gridDim.x) {
+    u32 s, slice;
+    if constexpr (RAGGED) {
+        if (w >= total)
+            return;
+        const u64 e = smap[w];
+        slice = u32(e);
+        s = g.order ? g.order[u32(e >> 32)] : u32(e >> 32);
+    } else {
+        s = w / slices;
+        slice = w % slices;
+        if (s >= g.nstripes)
+            return;
+    }
     const u8 *pl = plan + u64(s) * (K + K * K);
     const u32 sl0 = pl[0];
-    if (sl0 == 0xFF)
-        return;  // fewer than K distinct ids: status says -EINVAL, block untouched
-    const u32 B = g.block_size;
+    if (sl0 == 0xFF) {  // fewer than K distinct ids: status says -EINVAL, block untouched
+        if constexpr (RAGGED)
+            continue;
+        return;
+    }
+    const u32 B = RAGGED ? g.block_sizes[s] : g.block_size;
     const u32 ps = part_size_of(B, K);
+    const u64 ppitch = RAGGED ? (u64(ps) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1) : g.part_pitch;
     const u32 rbase = slice * R;
-    const u8 *pbase = g.parts + u64(s) * n_slots * g.part_pitch;
-    u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
+    const u8 *pbase = RAGGED ? g.parts + g.part_off[s] : g.parts + u64(s) * n_slots * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + (RAGGED ? g.block_off[s] : u64(s) * g.block_pitch);
+    // ragged part offsets are caller data: byte loads where a stripe's parts
+    // are not 16-byte aligned (uniform batches are checked by the launcher)
+    const bool pal = !RAGGED || (reinterpret_cast<uintptr_t>(pbase) & 15) == 0;
 
     // loads first (their latency hides under the table build)
     const u8 *src[K];
 #pragma unroll
     for (int c = 0; c < K; ++c)
-        src[c] = pbase + u64(c ? pl[c] : sl0) * g.part_pitch;
+        src[c] = pbase + u64(c ? pl[c] : sl0) * ppitch;
     u32 pv[U][K][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -606,11 +630,21 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
         if (r0 < ps)
 #pragma unroll
             for (int c = 0; c < K; ++c) {
-                const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
-                pv[u][c][0] = t.x;
-                pv[u][c][1] = t.y;
-                pv[u][c][2] = t.z;
-                pv[u][c][3] = t.w;
+                if (pal) {
+                    const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
+                    pv[u][c][0] = t.x;
+                    pv[u][c][1] = t.y;
+                    pv[u][c][2] = t.z;
+                    pv[u][c][3] = t.w;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        u32 x = 0;
+                        for (int e = 0; e < 4; ++e)
+                            x |= u32(src[c][r0 + 4 * q + e]) << (8 * e);  // within the pitch
+                        pv[u][c][q] = x;
+                    }
+                }
             }
     }
     // U_c[x] = (W[c][0] x, ..., W[c][K-1] x), packed
@@ -632,7 +666,7 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
     }
     __syncthreads();
 
-    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | g.block_pitch) & 15) == 0;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(out) | (RAGGED ? 0 : g.block_pitch)) & 15) == 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const u32 ru = rbase + u * 1024;  // first row of this unit
@@ -722,6 +756,58 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
             }
         }
     }
+    if constexpr (!RAGGED)
+        return;
+    __syncthreads();  // the next slice rebuilds the tables
+    }
+}
+
+// Exclusive prefix of the slices per stripe of a ragged batch in processing
+// order (g.order applied): sfirst[0..nstripes], *stotal = sfirst[nstripes].
+// One workgroup; every thread sums a contiguous run of stripes.
+__global__ __launch_bounds__(1024) void k_slice_scan(const u32 *sizes, const u32 *order, u32 nstripes, int k,
+                                                     u32 rows, u32 *sfirst, u32 *stotal)
+{
+    __shared__ u32 part[1024];
+    const u32 t = threadIdx.x;
+    const u32 per = (nstripes + 1023) / 1024;
+    const u32 a = min(nstripes, t * per), b = min(nstripes, a + per);
+    auto slices_of = [&](u32 p) {
+        const u32 ps = part_size_of(sizes[order ? order[p] : p], k);
+        return ps ? (ps + rows - 1) / rows : 1u;  // an empty stripe is one (empty) pass
+    };
+    u32 sum = 0;
+    for (u32 p = a; p < b; ++p)
+        sum += slices_of(p);
+    part[t] = sum;
+    __syncthreads();
+    for (u32 d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+        const u32 v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    u32 run = t ? part[t - 1] : 0u;
+    for (u32 p = a; p < b; ++p) {
+        sfirst[p] = run;
+        run += slices_of(p);
+    }
+    if (t == 1023) {
+        sfirst[nstripes] = part[1023];
+        *stotal = part[1023];
+    }
+}
+
+// smap[sfirst[p] + j] = (p << 32) | j for the slices j of the stripe at
+// processing position p: one wave per stripe, lanes over its slices.
+__global__ __launch_bounds__(256) void k_slice_map(const u32 *sfirst, u32 nstripes, u64 *smap)
+{
+    const u32 p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= nstripes)
+        return;
+    const u32 a = sfirst[p], n = sfirst[p + 1] - a;
+    for (u32 j = threadIdx.x & 63; j < n; j += 64)
+        smap[a + j] = (u64(p) << 32) | j;
 }
 
 // ----------------------------------------------------------------- launchers
@@ -810,53 +896,79 @@ extern "C" int nkfs_walk_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// uniform: one wave per (stripe, slice); ragged: a persistent grid of the
+// resident waves over the scanned slice list
 template <int K, int E, int U, bool XP>
-static void launch_slice(hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *plan, u32 slices, int waves)
+static void launch_slice(hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *plan, u32 slices, int waves,
+                         const u64 *smap, const u32 *stotal, int cus)
 {
-    const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_slice<K, E, U, XP>), waves);
-    hipLaunchKernelGGL((k_decode_slice<K, E, U, XP>), dim3(g.nstripes * slices), dim3(64), sh.pad, st, g, n_slots,
-                       plan, slices);
+    if (smap) {
+        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_slice<K, E, U, XP, true>), waves);
+        hipLaunchKernelGGL((k_decode_slice<K, E, U, XP, true>), dim3(u32(cus) * u32(sh.per_cu)), dim3(64), sh.pad,
+                           st, g, n_slots, plan, 0u, smap, stotal);
+        return;
+    }
+    const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_slice<K, E, U, XP, false>), waves);
+    hipLaunchKernelGGL((k_decode_slice<K, E, U, XP, false>), dim3(g.nstripes * slices), dim3(64), sh.pad, st, g,
+                       n_slots, plan, slices, (const u64 *)nullptr, (const u32 *)nullptr);
 }
 
 template <int K, int E>
 static void launch_slice_u(int units, hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *plan, u32 slices,
-                           int waves)
+                           int waves, const u64 *smap, const u32 *stotal, int cus)
 {
     constexpr bool XP = K >= 3;
     if (units >= 4)
-        launch_slice<K, E, 4, XP>(st, g, n_slots, plan, slices, waves);
+        launch_slice<K, E, 4, XP>(st, g, n_slots, plan, slices, waves, smap, stotal, cus);
     else if (units == 2)
-        launch_slice<K, E, 2, XP>(st, g, n_slots, plan, slices, waves);
+        launch_slice<K, E, 2, XP>(st, g, n_slots, plan, slices, waves, smap, stotal, cus);
     else
-        launch_slice<K, E, 1, XP>(st, g, n_slots, plan, slices, waves);
+        launch_slice<K, E, 1, XP>(st, g, n_slots, plan, slices, waves, smap, stotal, cus);
 }
 
-// Slice decoder for a uniform batch, k <= 8: plan kernel (selection +
-// inverse per stripe into `work`, nkfs_decode_work_bytes layout) then
-// one-shot slice waves.  -ENOSYS outside its shapes.
+// Slice decoder, k <= 8: plan kernel (selection + inverse per stripe into
+// `work`, nkfs_decode_work_bytes layout) then one-shot slice waves; a ragged
+// batch (g->order honoured) first scans its slice counts into stream-ordered
+// scratch.  -ENOSYS outside its shapes.
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
                                  int navail, void *work, int32_t *status, const void *gf, int units, int waves,
-                                 hipStream_t st)
+                                 int cus, hipStream_t st)
 {
-    if (g->k > 8 || g->block_sizes || (g->part_pitch & 15) || (reinterpret_cast<uintptr_t>(g->parts) & 15))
+    if (g->k > 8 || (reinterpret_cast<uintptr_t>(g->parts) & 15) || (!g->block_sizes && (g->part_pitch & 15)))
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
     u8 *plan = static_cast<u8 *>(work);
     const GfTables *gft = static_cast<const GfTables *>(gf);
     const dim3 pgrid((g->nstripes + 255) / 256);
-    const u32 ps = part_size_of_host(g->block_size, g->k);
+    const u32 ps = part_size_of_host(g->block_size, g->k);  // ragged: the bound on block sizes
     units = units >= 4 ? 4 : units >= 2 ? 2 : 1;
     // a stripe that fits in fewer units takes one wave of just those
-    while (units > 1 && u32(units / 2) * 1024u >= ps)
+    while (!g->block_sizes && units > 1 && u32(units / 2) * 1024u >= ps)
         units /= 2;
     const u32 slices = (ps + 1024u * units - 1) / (1024u * units);
+    // ragged: slice list in stream-ordered scratch -- nstripes + 2 u32 of
+    // prefix and total, then at most nstripes * slices(max) u64 map entries
+    u32 *scan = nullptr;
+    u64 *smap = nullptr;
+    if (g->block_sizes) {
+        const size_t head = ((size_t(g->nstripes) + 2) * sizeof(u32) + 15) & ~size_t(15);
+        if (hipMallocAsync(reinterpret_cast<void **>(&scan), head + size_t(g->nstripes) * slices * sizeof(u64), st) !=
+            hipSuccess)
+            return -ENOSYS;
+        smap = reinterpret_cast<u64 *>(reinterpret_cast<u8 *>(scan) + head);
+        hipLaunchKernelGGL(k_slice_scan, dim3(1), dim3(1024), 0, st, g->block_sizes, g->order, g->nstripes, g->k,
+                           1024u * u32(units), scan, scan + g->nstripes + 1);
+        hipLaunchKernelGGL(k_slice_map, dim3((g->nstripes + 3) / 4), dim3(256), 0, st, scan, g->nstripes, smap);
+    }
+    const u32 *stotal = scan ? scan + g->nstripes + 1 : nullptr;
+    int rc = 0;
     switch (g->k) {
 #define NKFS_DK(KK, EE)                                                                                          \
     case KK:                                                                                                     \
         hipLaunchKernelGGL((k_decode_plan<KK>), pgrid, dim3(256), 0, st, ids, avail, n_slots, navail, g->nstripes, \
                            plan, status, gft);                                                                   \
-        launch_slice_u<KK, EE>(units, st, *g, n_slots, plan, slices, waves);                                     \
+        launch_slice_u<KK, EE>(units, st, *g, n_slots, plan, slices, waves, smap, stotal, cus);                  \
         break;
         NKFS_DK(2, 4)
         NKFS_DK(3, 4)
@@ -867,7 +979,11 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         NKFS_DK(8, 8)
 #undef NKFS_DK
     default:
-        return -ENOSYS;
+        rc = -ENOSYS;
     }
+    if (scan && hipFreeAsync(scan, st) != hipSuccess && !rc)
+        rc = -EIO;
+    if (rc)
+        return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
