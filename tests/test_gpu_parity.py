@@ -738,3 +738,49 @@ def test_ragged_kernels_match(L, O, n, k, gap, order):
         B = int(sizes[s])
         want = _oracle_digests(O, hb[None, boff[s]: boff[s] + B], rid[s:s + 1], n, k, B)
         assert got[s * n:(s + 1) * n] == want, (s, B)
+
+
+@pytest.mark.parametrize("n,k,units", [(8, 5, 2), (6, 3, 4), (8, 8, 1)])
+def test_ragged_slice_decode_matches_wave(L, n, k, units):
+    """Ragged batches on the slice decoder (persistent grid over the scanned
+    (stripe, slice) map, size order) rebuild the same blocks and statuses as
+    the wave decoder, with part regions at unaligned offsets (byte loads),
+    output blocks at unaligned offsets, one-byte and k+1-byte stripes, and a
+    stripe offering too few distinct ids (-EINVAL, block untouched)."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(30)
+    sizes[:5] = (1048576, 1, k + 1, 4096 + 3, 65536)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, 5)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(40 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=40)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff),
+                        None, int(sizes.max()))
+    # the same parts at offsets shifted by 0..7 bytes per stripe
+    shift = np.arange(len(sizes), dtype=np.int64) % 8
+    poff2 = poff + np.cumsum(shift)
+    parts2 = torch.zeros(ppos + int(shift.sum()) + 16, dtype=torch.uint8, device="cuda")
+    for s, B in enumerate(sizes):
+        ln = n * batch.part_pitch(int(B), k)
+        parts2[poff2[s]: poff2[s] + ln] = parts[poff[s]: poff[s] + ln]
+    avail = synth.batch_survivors(len(sizes), n, k, first=40)
+    ids2 = ids_np.copy()
+    ids2[3, :] = ids2[3, 0]  # stripe 3: one distinct id
+    outs = []
+    for kern, pp, po in (("wave", parts, poff), ("slice", parts, poff), ("slice", parts2, poff2)):
+        with _tuned(dec_kernel=_dec(kern), dec_units=units):
+            out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+            st = batch.decode_ragged(pp, dev(po), n, dev(ids2), dev(avail), k, out, dev(boff),
+                                     dev(sizes.astype(np.int32)), int(sizes.max()))
+            torch.cuda.synchronize()
+            outs.append((out.cpu(), st.cpu().tolist()))
+    for o, st in outs[1:]:
+        assert st == outs[0][1]
+        assert torch.equal(o, outs[0][0])
+    o, st = outs[0]
+    assert st[3] == -22 and bool((o[boff[3]: boff[3] + sizes[3]] == 0xEE).all())
+    for s, B in enumerate(sizes):
+        if s != 3:
+            assert st[s] == 0 and np.array_equal(o[boff[s]: boff[s] + B].numpy(), host[boff[s]: boff[s] + B]), s
