@@ -1,26 +1,32 @@
 """bench.py -- device-resident N-K encode(+XXH64 of every part)+decode
-throughput on MI355X, one process per GPU, weak scaling over stripes.
+throughput on MI355X, one process per GPU, stripes partitioned over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config all|c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config all|c2|c3|c4|c5|w1|w2]
+                    [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Headline (BASELINE.json metric, configs[2] = SURVEY.md §8(d) C3): N=8, K=5,
-1 MiB stripes, 8,192 stripes (8 GiB) per GPU.  Step = one pass of the hot
-path over the batch resident in HBM:
+1 MiB stripes, 8,192 stripes (8 GiB) in all, split evenly over the GPUs
+(strong scaling, as SURVEY.md §8(d) defines C3; --scaling weak keeps 8,192
+per GPU).  Step = one pass of the hot path over the batch resident in HBM:
   nkfs_nk8_encode  (fused encode + XXH64 of every part), then
   nkfs_nk8_decode  (per-stripe K x K inverse + apply) from the seeded
                    survivors (n-k parts erased per stripe).
-value = user bytes of all ranks x K steps / max-over-ranks wall time (GiB/s).
+value = user bytes of the whole job x K steps / max-over-ranks wall time.
 
-The same line carries the other BASELINE configs as sub-objects under
-"configs" (C2: 65,536 x 4 KiB N4K2; C4: 16,384 x 256 KiB N8K5; C5: the
-ragged 4 KiB / 64 KiB / 1 MiB mix, byte-balanced over the ranks), each
-timed over at least 200 ms with its own roofline and CPU baseline.
+The same line carries the other configs as sub-objects under "configs"
+(c3s8: the 1,024-stripe per-GPU shard of the strong N=8 run, timed on one
+GPU; C2: 65,536 x 4 KiB N4K2; C4: 16,384 x 256 KiB N8K5; C5: the ragged
+4 KiB / 64 KiB / 1 MiB mix, byte-balanced over the ranks; W1/W2: the general
+n, k paths), each timed over at least 200 ms with its own roofline.
 
 The dominant kernel's roofline is measured live with HIP events on the
 stream the library launches on (torch's current stream); algorithmic bytes
-per stripe are SURVEY.md §8(d)'s: encode+hash B + n*ps + 8n.  The CPU
-baseline (rank 0, N=1) times the reference's own code (oracle/_ref) on a
+per stripe are SURVEY.md §8(d)'s: encode+hash B + n*ps + 8n.  Next to the
+8 TB/s spec every roofline carries `box_stream`: the rate this box sustains,
+in the same process, for the kernel's read:write mix with the arithmetic
+stripped (nkfs_amd/csrc/boxprobe.hip), and the kernel's fraction of it.  The
+CPU baseline (rank 0, N=1) times the reference's own code (oracle/_ref) on a
 bounded sample of the same workload on this box's host cores: one thread
 and the box's CPU share.
 """
@@ -50,6 +56,10 @@ CONFIGS = {
     # part-group encoder and survivor-table decoder (nk8_wide.hip); XXH64 is a second pass over the parts
     "w1": (2048, 1048576, 16, 12, "W1: N=16,K=12 encode(+XXH64/part)+decode(4 erased), 2048 x 1 MiB stripes per "
                                   "GPU (general n,k path; not a BASELINE config)"),
+    # k > 16 (the reference allows k <= 254, crt/nk8.c:13-16; its self test draws k uniform in [2, 254],
+    # crt/nk8.c:735-744): the general-k kernels
+    "w2": (256, 1048576, 48, 32, "W2: N=48,K=32 encode(+XXH64/part)+decode(16 erased), 256 x 1 MiB stripes per "
+                                 "GPU (k > 16 path; not a BASELINE config)"),
     # ragged: block size of every stripe drawn from C5_SIZES (synth.mixed_sizes)
     "c5": (11520, None, 8, 5, "C5: N=8,K=5 encode(+XXH64/part)+decode(3 erased) of a ragged batch, stripe sizes "
                               "uniform over {4 KiB, 64 KiB, 1 MiB}, ~4 GiB per GPU, byte-balanced over the GPUs"),
@@ -68,6 +78,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time the host-memory (PCIe-inclusive) path")
     ap.add_argument("--stripes", type=int, default=0, help="override the stripes per GPU of a single --config")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="headline C3: strong = 8,192 stripes in all split over the GPUs (SURVEY.md §8(d)); "
+                         "weak = 8,192 per GPU")
     return ap.parse_args()
 
 
@@ -88,6 +101,15 @@ def dist_setup(backend: str):
 def stripe_range(rank: int, per_rank: int):
     """Rank r owns stripes [r*per_rank, (r+1)*per_rank) (weak scaling)."""
     return rank * per_rank, per_rank
+
+
+def strong_range(rank: int, world: int, total: int):
+    """Strong scaling (8,192 stripes total split evenly
+    across the G GPUs): rank r owns the contiguous range [lo, hi) of the
+    global batch, sizes differing by at most one stripe."""
+    lo = total * rank // world
+    hi = total * (rank + 1) // world
+    return lo, hi - lo
 
 
 def byte_balanced_ranges(sizes, world: int):
@@ -203,6 +225,63 @@ def auto_steps(step, device, min_steps):
     return max(min_steps, int(math.ceil(MIN_TIMED_S / est)))
 
 
+_PROBE = None
+
+
+def probe_lib():
+    """nkfs_amd/lib/libnkfs_boxprobe.so (nkfs_amd/csrc/boxprobe.hip): the
+    arithmetic-free stream bench.py calibrates each box with; None if absent."""
+    global _PROBE
+    if _PROBE is None:
+        import ctypes as C
+        path = os.path.join(ROOT, "nkfs_amd", "lib", "libnkfs_boxprobe.so")
+        if not os.path.exists(path):
+            return None
+        P = C.CDLL(path)
+        P.nkfs_probe_stream.restype = C.c_int
+        P.nkfs_probe_stream.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_double)]
+        _PROBE = P
+    return _PROBE
+
+
+MIXES = ((4, 8), (5, 8), (6, 8), (8, 8), (8, 4))
+
+
+def box_stream(src, dst, read_bytes, write_bytes, stream):
+    """HBM rate (GB/s) this box sustains, in this process, for the kernel's
+    read:write mix with the arithmetic stripped: contiguous 1 KiB runs, a
+    compact chip-wide front, 8 and 16 resident waves per CU (the better one
+    is kept).  `src` / `dst` are the kernel's own input / output tensors
+    (their contents are overwritten: call after verification).  The spec
+    peak is 8 TB/s; this is the ceiling the box really offers the mix."""
+    import ctypes as C
+    P = probe_lib()
+    if P is None:
+        return None
+    ratio = read_bytes / max(1, write_bytes)
+    L, S = min(MIXES, key=lambda c: abs(c[0] / c[1] - ratio))
+    best = 0.0
+    for wpc in (8, 16):
+        ms, nb = C.c_float(0), C.c_double(0)
+        rc = P.nkfs_probe_stream(src.data_ptr(), src.numel() * src.element_size(), dst.data_ptr(),
+                                 dst.numel() * dst.element_size(), L, S, wpc, 9, stream.cuda_stream, C.byref(ms),
+                                 C.byref(nb))
+        if rc == 0 and ms.value > 0:
+            best = max(best, nb.value / (ms.value * 1e-3) / 1e9)
+    if best <= 0:
+        return None
+    return {"GBps": round(best, 1), "read_write_kib": [L, S], "frac_of_peak": round(best / HBM_PEAK_GBS, 4)}
+
+
+def with_box(roof, box):
+    """Attach the box's own stream ceiling to a roofline dict."""
+    if box:
+        roof["box_stream"] = box
+        roof["frac_of_box_stream"] = round(roof["achieved"] / box["GBps"], 4)
+    return roof
+
+
 def roofline(kernel, nbytes, secs, traffic):
     return {"bound": "hbm", "kernel": kernel, "achieved": round(nbytes / secs / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(nbytes / secs / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -211,15 +290,25 @@ def roofline(kernel, nbytes, secs, traffic):
 
 # --------------------------------------------------------------- workload
 
-def run_uniform(name, args, rank, world, device, steps, stripes=0):
-    """One uniform config: returns the result dict (value, roofline, ...)."""
+def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=0):
+    """One uniform config: returns the result dict (value, roofline, ...).
+    Weak scaling: `stripes` (default the config's) per GPU.  Strong scaling
+    (strong_total > 0): that many stripes in all, split over the ranks."""
     import torch
     from nkfs_amd import batch, synth
     S, B, n, k, desc = CONFIGS[name]
-    if stripes:
-        S = stripes
-        desc = f"{desc.split(', ')[0]}, {desc.split(', ')[1]}, {S} x {B // 1024} KiB stripes per GPU"
-    first, _ = stripe_range(rank, S)
+    head = f"{desc.split(', ')[0]}, {desc.split(', ')[1]}"
+    if strong_total:
+        first, S = strong_range(rank, world, strong_total)
+        desc = (f"{head}, {strong_total} x {B // 1024} KiB stripes in all, split evenly over {world} GPU(s) "
+                f"(strong scaling; {S} on this GPU)")
+        world_bytes_scale = None
+    else:
+        if stripes:
+            S = stripes
+            desc = f"{head}, {S} x {B // 1024} KiB stripes per GPU"
+        first, _ = stripe_range(rank, S)
+        world_bytes_scale = world
     ps = batch.part_size(B, k)
     stream = torch.cuda.current_stream(device)
 
@@ -264,23 +353,32 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0):
     ranks_ok = None
     if rank == 0:
         def expect(r, s):
-            g = r * S + s
+            g = (strong_range(r, world, strong_total)[0] if strong_total else r * S) + s
             return [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
         ranks_ok = check_rank_digests(all_dig, n, expect)
     ok &= ranks_ok != -1
     enc_bytes = S * (B + n * ps + 8 * n)
     dec_bytes = S * (k * ps + B + k)
-    user_bytes = S * B * world * steps
+    # user bytes of the whole job: weak = every rank's S; strong = the total
+    total_stripes = strong_total if strong_total else S * world_bytes_scale
+    user_bytes = total_stripes * B * steps
+    # the box's own ceiling for each kernel's read:write mix, on the
+    # kernel's own buffers (after verification: the probe overwrites them)
+    box_enc = box_stream(blocks, parts, S * B, S * n * ps, stream)
+    box_dec = box_stream(parts, out, S * k * ps, S * B, stream)
+    dec = with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
+                    "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4), "us_per_launch": round(dec_s * 1e6, 2),
+                    "bytes_per_launch": dec_bytes}, box_dec)
     res = {
         "value": round(user_bytes / elapsed / 2**30, 3), "unit": "GiB/s", "steps": steps,
         "ms_per_step": round(elapsed / steps * 1e3, 4), "timed_ms": round(elapsed * 1e3, 1),
+        "scaling": "strong" if strong_total else "weak",
         "config": {"workload": desc, "n": n, "k": k, "block_size": B, "stripes_per_gpu": S, "part_size": ps,
-                   "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}"},
-        "roofline": roofline("nkfs_nk8_encode (encode + XXH64 per part)", enc_bytes, enc_s,
-                             pmc_traffic(name) if not stripes else None),
-        "decode": {"achieved_GBps": round(dec_bytes / dec_s / 1e9, 1), "frac": round(dec_bytes / dec_s / 1e9 /
-                                                                                     HBM_PEAK_GBS, 4),
-                   "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes},
+                   "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}",
+                   "stripes_all_gpus": total_stripes},
+        "roofline": with_box(roofline("nkfs_nk8_encode (encode + XXH64 per part)", enc_bytes, enc_s,
+                                      pmc_traffic(name, S, world)), box_enc),
+        "decode": dec,
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -384,17 +482,20 @@ def run_ragged(args, rank, world, device, steps):
     enc_bytes = user + n * sum(ps) + 8 * n * S
     dec_bytes = k * sum(ps) + user + k * S
     total_user = reduce_sum(user, device)
+    box_enc = box_stream(blocks, parts, user, n * sum(ps), stream)
+    box_dec = box_stream(parts, out, k * sum(ps), user, stream)
     res = {
         "value": round(total_user * steps / elapsed / 2**30, 3), "unit": "GiB/s", "steps": steps,
         "ms_per_step": round(elapsed / steps * 1e3, 4), "timed_ms": round(elapsed * 1e3, 1),
         "config": {"workload": desc, "n": n, "k": k, "block_sizes": list(C5_SIZES), "stripes_this_gpu": S,
                    "user_bytes_this_gpu": user, "user_bytes_all_gpus": total_user, "erased_per_stripe": n - k,
                    "parallelism": f"stripe-partition x{world} (byte-balanced ranges)"},
-        "roofline": roofline("nkfs_nk8_encode_ragged (encode + XXH64 per part)", enc_bytes, enc_s,
-                             pmc_traffic("c5") if world == 1 else None),
-        "decode": {"achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
-                   "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4),
-                   "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes},
+        "scaling": "weak",
+        "roofline": with_box(roofline("nkfs_nk8_encode_ragged (encode + XXH64 per part)", enc_bytes, enc_s,
+                                      pmc_traffic("c5", None, world)), box_enc),
+        "decode": with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
+                            "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4),
+                            "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes}, box_dec),
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -432,17 +533,26 @@ def main():
     _lib.check(L.nkfs_gpu_init(local), "nkfs_gpu_init")
 
     head = HEADLINE if args.config == "all" else args.config
-    run = (lambda name, steps: run_ragged(args, rank, world, device, steps) if name == "c5"
-           else run_uniform(name, args, rank, world, device, steps, args.stripes if args.config != "all" else 0))
-    top = run(head, args.steps)
+    strong = CONFIGS[HEADLINE][0] if (args.scaling == "strong" and head == HEADLINE and not args.stripes) else 0
+
+    def run(name, steps, stripes=0, strong_total=0):
+        if name == "c5":
+            return run_ragged(args, rank, world, device, steps)
+        return run_uniform(name, args, rank, world, device, steps, stripes, strong_total)
+
+    top = run(head, args.steps, args.stripes if args.config != "all" else 0, strong)
     subs = {}
     if args.config == "all":
-        for name in ("c2", "c4", "c5", "w1"):
+        if world == 1:
+            # the per-GPU shard of the headline's strong N=8 run, timed on one
+            # GPU now (kernel choice and per-GPU efficiency at 1,024 stripes)
+            subs["c3s8"] = run("c3", None, CONFIGS["c3"][0] // 8)
+        for name in ("c2", "c4", "c5", "w1", "w2"):
             subs[name] = run(name, None)
     result = {
         "metric": METRIC, "value": top.pop("value"), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": top.pop("ms_per_step"), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8",
+        "warmup": args.warmup, "ms_per_step": top.pop("ms_per_step"), "higher_is_better": True,
+        "scaling": top.pop("scaling"), "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846)",
     }
     top.pop("steps")
@@ -542,16 +652,21 @@ def cpu_baseline_mixed(sizes, n, k, target_s):
                       f"~{target_s:.0f} s per thread count"}
 
 
-def pmc_traffic(config):
+def pmc_traffic(config, stripes=None, world=1):
     """Per-launch HBM bytes of the encode kernel from the committed rocprofv3
     PMC summary (tools/pmc.sh: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    FETCH_SIZE halving corrected per MI355X_MICROARCH.md §HBM), or None."""
+    FETCH_SIZE halving corrected per MI355X_MICROARCH.md §HBM), or None.
+    Attached only to a line whose per-GPU stripe count is the profiled
+    run's and that runs on one GPU (the PMC pass is a 1-GPU run)."""
+    if world != 1:
+        return None
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             entry = json.load(f).get(config)
         # measured on this config's own batch only (tools/pmc.sh records it)
-        if entry is None or entry.get("stripes") != CONFIGS[config][0]:
+        want = CONFIGS[config][0] if stripes is None else stripes
+        if entry is None or entry.get("stripes") != want:
             return None
         return entry["encode_bytes_per_launch"]
     except (OSError, ValueError, KeyError):

@@ -1,0 +1,140 @@
+// boxprobe.hip -- measurement helper for bench.py (not part of the product
+// library): the HBM rate THIS box sustains for a given read:write mix with
+// the arithmetic stripped, so every bench line can state its kernel's
+// fraction of the box's own ceiling next to the fraction of the 8 TB/s spec.
+//
+// Why: the encode/decode kernels are HBM-mix-bound.  Measured across boxes
+// (profiles/r03/sol3_*.txt) a pure read stream runs 6.0-6.3 TB/s and a pure
+// write stream 5.0-6.3, but a 5:8 read:write mix (the N8K5 encode's) only
+// 5.1-5.7 TB/s depending on the box; the spread between boxes is larger
+// than any kernel change measured this round.
+//
+// k_mix<L,S>: persistent grid, one wave per workgroup; step t of wave w
+// loads L KiB (one contiguous 1 KiB run per instruction) from chunk t*G + w
+// of the input and stores S KiB to the same chunk of the output (compact
+// chip-wide front: the fastest arrangement measured); the next step's loads
+// issue before this step's stores.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stddef.h>
+#include <stdint.h>
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+namespace {
+
+template <int L, int S>
+__global__ __launch_bounds__(64) void k_mix(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 nsteps)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t pad[];
+    const int li = threadIdx.x;
+    const u32 G = gridDim.x;
+    v4u d[2][L];
+    auto load = [&](v4u (&x)[L], u32 t) {
+        const u64 base = t < nsteps ? (u64(t) * G + blockIdx.x) * (L * 1024u) : 0;
+#pragma unroll
+        for (int q = 0; q < L; ++q)
+            x[q] = *reinterpret_cast<const v4u *>(in + base + q * 1024 + li * 16);
+    };
+    auto store = [&](v4u (&x)[L], u32 t) {
+        uint8_t *p = out + (u64(t) * G + blockIdx.x) * (S * 1024u);
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            v4u v = x[q % L];
+            v.x ^= u32(q);
+            *reinterpret_cast<v4u *>(p + q * 1024 + li * 16) = v;
+        }
+    };
+    load(d[0], 0);
+    for (u32 t = 0; t < nsteps; t += 2) {
+        load(d[1], t + 1);
+        store(d[0], t);
+        if (t + 1 >= nsteps)
+            break;
+        load(d[0], t + 2);
+        store(d[1], t + 1);
+    }
+}
+
+template <int L, int S>
+int run(const void *in, size_t in_bytes, void *out, size_t out_bytes, int waves_per_cu, int reps, hipStream_t st,
+        float *ms, double *bytes)
+{
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return -ENODEV;
+    const u32 G = u32(cus) * u32(waves_per_cu);
+    const u64 steps = in_bytes / (u64(L) * 1024u * G) < out_bytes / (u64(S) * 1024u * G)
+                          ? in_bytes / (u64(L) * 1024u * G)
+                          : out_bytes / (u64(S) * 1024u * G);
+    if (steps < 2 || steps > 0xFFFFFFFFull)
+        return -EINVAL;
+    // dynamic LDS that caps residency at waves_per_cu one-wave workgroups
+    size_t lds = 160u * 1024u / size_t(waves_per_cu);
+    if (lds > 65536)
+        lds = 65536;
+    auto kern = k_mix<L, S>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            65536) != hipSuccess)
+        return -EIO;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess)
+        return -EIO;
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return -EIO;
+    }
+    float t[33];
+    if (reps > 33)
+        reps = 33;
+    if (reps < 1)
+        reps = 1;
+    int rc = 0;
+    hipLaunchKernelGGL(kern, dim3(G), dim3(64), lds, st, (const uint8_t *)in, (uint8_t *)out, u32(steps));
+    for (int r = 0; r < reps && !rc; ++r) {
+        (void)hipEventRecord(e0, st);
+        hipLaunchKernelGGL(kern, dim3(G), dim3(64), lds, st, (const uint8_t *)in, (uint8_t *)out, u32(steps));
+        (void)hipEventRecord(e1, st);
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t[r], e0, e1) != hipSuccess)
+            rc = -EIO;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc)
+        return rc;
+    for (int a = 0; a < reps; ++a)
+        for (int b = a + 1; b < reps; ++b)
+            if (t[b] < t[a]) {
+                const float x = t[a];
+                t[a] = t[b];
+                t[b] = x;
+            }
+    *ms = t[reps / 2];
+    *bytes = double(steps) * G * 1024.0 * (L + S);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+}  // namespace
+
+// Median time (ms) of `reps` launches streaming the read:write mix
+// read_kib:write_kib (one of 4:8, 5:8, 6:8, 8:8, 8:4) from `in` to `out` at
+// waves_per_cu resident waves per CU, and the bytes one launch moves.
+extern "C" int nkfs_probe_stream(const void *in, size_t in_bytes, void *out, size_t out_bytes, int read_kib,
+                                 int write_kib, int waves_per_cu, int reps, hipStream_t st, float *ms, double *bytes)
+{
+    if (!in || !out || !ms || !bytes || waves_per_cu < 1 || waves_per_cu > 32)
+        return -EINVAL;
+#define NKFS_MIX(LL, SS)                                                                              \
+    if (read_kib == LL && write_kib == SS)                                                            \
+        return run<LL, SS>(in, in_bytes, out, out_bytes, waves_per_cu, reps, st, ms, bytes);
+    NKFS_MIX(4, 8)
+    NKFS_MIX(5, 8)
+    NKFS_MIX(6, 8)
+    NKFS_MIX(8, 8)
+    NKFS_MIX(8, 4)
+#undef NKFS_MIX
+    return -EINVAL;
+}

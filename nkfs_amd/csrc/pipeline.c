@@ -53,8 +53,11 @@ static struct pin_ent *g_pins;
 /* Pin [p, p+bytes) for a call: memory the runtime already knows as pinned
  * (hipHostMalloc, torch pinned memory, a range someone else registered)
  * needs nothing; a range inside one this registry holds takes a reference;
- * anything else is registered here with one reference.  *held = the entry
- * to release (NULL when nothing was taken). */
+ * a range that overlaps this registry's entries without lying inside one of
+ * them is refused (-EBUSY: the entry's owner could unpin it mid-copy, and
+ * the runtime would report the range as pinned); anything else is
+ * registered here with one reference.  *held = the entry to release (NULL
+ * when nothing was taken). */
 static int pin_take(const void *p, size_t bytes, struct pin_ent **held)
 {
 	*held = NULL;
@@ -63,12 +66,25 @@ static int pin_take(const void *p, size_t bytes, struct pin_ent **held)
 	const uintptr_t a = (uintptr_t)p;
 	int rc = 0;
 	pthread_mutex_lock(&g_pin_lock);
-	for (struct pin_ent *e = g_pins; e; e = e->next)
+	struct pin_ent *inside = NULL;
+	int overlaps = 0;
+	for (struct pin_ent *e = g_pins; e; e = e->next) {
 		if (a >= e->base && a + bytes <= e->base + e->bytes) {
-			e->refs++;
-			*held = e;
-			goto out;
+			inside = e;
+			break;
 		}
+		if (a < e->base + e->bytes && e->base < a + bytes)
+			overlaps = 1;
+	}
+	if (inside) {
+		inside->refs++;
+		*held = inside;
+		goto out;
+	}
+	if (overlaps) {
+		rc = -EBUSY;
+		goto out;
+	}
 	hipPointerAttribute_t attr;
 	if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) {
 		/* pinned by its owner; a range that only starts inside such an
@@ -101,11 +117,9 @@ out:
 	return rc;
 }
 
-static void pin_drop(struct pin_ent *e)
+/* caller holds g_pin_lock */
+static void pin_drop_locked(struct pin_ent *e)
 {
-	if (!e)
-		return;
-	pthread_mutex_lock(&g_pin_lock);
 	if (--e->refs == 0) {
 		for (struct pin_ent **pp = &g_pins; *pp; pp = &(*pp)->next)
 			if (*pp == e) {
@@ -115,6 +129,14 @@ static void pin_drop(struct pin_ent *e)
 		hipHostUnregister((void *)e->base);
 		free(e);
 	}
+}
+
+static void pin_drop(struct pin_ent *e)
+{
+	if (!e)
+		return;
+	pthread_mutex_lock(&g_pin_lock);
+	pin_drop_locked(e);
 	pthread_mutex_unlock(&g_pin_lock);
 }
 
@@ -131,15 +153,16 @@ int nkfs_host_register(void *p, size_t bytes)
 
 int nkfs_host_unregister(void *p)
 {
+	/* lookup and release in one locked section: a concurrent drop cannot
+	 * free the entry in between */
 	pthread_mutex_lock(&g_pin_lock);
 	struct pin_ent *e = g_pins;
 	while (e && e->base != (uintptr_t)p)
 		e = e->next;
+	if (e)
+		pin_drop_locked(e);
 	pthread_mutex_unlock(&g_pin_lock);
-	if (!e)
-		return -ENOENT;
-	pin_drop(e);
-	return 0;
+	return e ? 0 : -ENOENT;
 }
 
 /* ------------------------------------------------------- batch description */

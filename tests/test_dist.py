@@ -28,6 +28,7 @@ def _worker(rank, world, port, q):
     r, w, local = bench.dist_setup("gloo")
     dev = torch.device("cpu")
     first, count = bench.stripe_range(r, 65536)
+    strong = bench.strong_range(r, w, 8192)
     t = bench.reduce_max(1.0 + r, dev)
     xs = bench.gather_digest_xor((0xF000_0000_0000_0000 | r), dev)
     # per-part digests of this rank's stripes, as the device would produce
@@ -72,7 +73,12 @@ def _worker(rank, world, port, q):
     ok5 = bench.check_rank_digests(g5, n5, expect5, samples=100) if r == 0 else None
     counts5 = [len(x) // n5 for x in g5]
     bench.barrier()
-    q.put((r, w, local.numel(), first, count, t, xs, ok, nok, ok5, counts5, ranges))
+    # strong scaling (C3: 8,192 stripes in all): every rank's global stripe
+    # indices, all-gathered, must tile [0, 8192) exactly once
+    mine_s = torch.arange(strong[0], strong[0] + strong[1], dtype=torch.int64)
+    all_s = bench.gather_digests(mine_s, dev)
+    tiled = sorted(int(x) for t_ in all_s for x in t_.tolist()) == list(range(8192))
+    q.put((r, w, local.numel(), first, count, t, xs, ok, nok, ok5, counts5, ranges, strong, tiled))
     dist.destroy_process_group()
 
 
@@ -88,7 +94,8 @@ def test_two_rank_gloo():
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    for r, (rank, world, nd, first, count, t, xs, ok, nok, ok5, counts5, ranges) in enumerate(res):
+    for r, (rank, world, nd, first, count, t, xs, ok, nok, ok5, counts5, ranges, strong, tiled) in enumerate(res):
+        assert strong == (r * 4096, 4096) and tiled
         assert (rank, world, nd) == (r, 2, 16)
         if r == 0:
             assert ok == 2 and nok == -1 and ok5 == 2
@@ -104,6 +111,18 @@ def test_single_rank_defaults(monkeypatch):
     assert bench.dist_setup("gloo") == (0, 1, 0)
     assert bench.reduce_max(3.5, torch.device("cpu")) == 3.5
     assert bench.gather_digest_xor(7, torch.device("cpu")) == [7]
+
+
+def test_strong_ranges():
+    """C3 strong scaling: the total is split into contiguous,
+    disjoint ranges covering it, sizes within one stripe."""
+    for total in (8192, 8191, 7, 1):
+        for world in (1, 2, 4, 8):
+            rs = [bench.strong_range(r, world, total) for r in range(world)]
+            assert rs[0][0] == 0 and sum(c for _, c in rs) == total
+            assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            assert max(c for _, c in rs) - min(c for _, c in rs) <= 1
+    assert bench.strong_range(7, 8, 8192) == (7168, 1024)
 
 
 def test_byte_balanced_ranges():
