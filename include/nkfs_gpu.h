@@ -58,10 +58,12 @@ int nkfs_gpu_get_devices(int *devices, int max);
  * them with nkfs_tune_set to compare kernels in one process.  The launchers
  * read only this struct: no environment variable changes what runs. */
 /* NKFS_ENC_WIDE: part-group encoder (any n, k <= 16; the default beyond the
- * fused kernels' n <= 8, k <= 8); NKFS_ENC_GENERIC: thread-per-row kernel */
-enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE };
-/* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16) */
-enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE };
+ * fused kernels' n <= 8, k <= 8); NKFS_ENC_GENERIC: thread-per-row kernel;
+ * NKFS_ENC_BIG: column-chunked encoder (any k; the default for k > 16) */
+enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG };
+/* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16);
+ * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16) */
+enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG };
 struct nkfs_tune {
 	int enc_kernel;       /* NKFS_ENC_*: encoder (WIDE / GENERIC also pin n <= 8 shapes) */
 	int dec_kernel;       /* NKFS_DEC_*: decoder (WIDE / GENERIC also pin k <= 8) */
@@ -75,8 +77,12 @@ struct nkfs_tune {
 	int enc_fused_waves_per_cu; /* fused encoder: resident waves per CU cap (0 = none, 3..32) */
 	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
 };
-void nkfs_tune_get(struct nkfs_tune *t);
-int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields */
+void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
+int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */
+/* 1 when every buffer offset the walk encoder forms for this shape fits 31
+ * bits (block bytes + a chunk's reach, a stripe's part span, the digest
+ * array), else 0: the launcher then takes the general kernels. */
+int nkfs_walk_offsets_fit(uint64_t block_size, uint64_t part_span, uint64_t nstripes, uint64_t n);
 
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */
 uint32_t nkfs_part_size(uint32_t block_size, int k);

@@ -2,34 +2,55 @@
  * csum.c -- the reference's checksum ABI (crt/include/csum.h:14-17,
  * crt/include/xxhash.h:86-132; XXH32 is not on the path and not exported)
  * with the XXH64 rounds, merge, tail and avalanche computed on the GPU
- * (k_xxh64_stripes / k_xxh64_finish in nk8_kernels.hip).
+ * (k_xxh64_chain, xxh64_chain.hip: one wave, the message's four serial
+ * chains at round latency, reading the staged bytes from pinned host memory).
  *
  * The state keeps the reference's internal layout (crt/xxhash.c:515-525)
  * inside the caller-owned 88-byte XXH64_state_t, and the host side does what
  * the reference's update does with memory: it buffers an incomplete 32-byte
- * stripe in mem64 (crt/xxhash.c:750-770, 823-833).  Each update that
- * completes at least one stripe ships the stripes and the four accumulators
- * to the device, folds them there and brings the accumulators back.
+ * stripe in mem64 (crt/xxhash.c:750-770, 823-833).
+ *
+ * One GPU round trip per message.  XXH64_update does not wait for the GPU:
+ * whole stripes are copied into pinned staging of a per-message context
+ * (stream + staging + device accumulators) held in a slot; every full
+ * 256 KiB of staging is folded by an asynchronous launch (accumulators stay
+ * on the device), so a long stream overlaps the host's copy with the GPU's
+ * chains.  XXH64_digest launches the last fold together with merge, tail
+ * and avalanche and spins on a completion word the kernel stores to host
+ * memory -- no stream synchronisation -- then writes the accumulators back
+ * into the state (the reference's state after the same updates) and frees
+ * the slot.  XXH64() / csum_* are reset + update + digest: one launch for
+ * messages up to 256 KiB.
+ *
+ * While a message is pending, the state's padding word (offset 84 of the
+ * 88 bytes, unused by the reference layout) holds the slot, and v[0] a
+ * 64-bit token of it; byte-copying a pending state and continuing both
+ * copies is not supported (the copy that digests second traps like
+ * CRT_BUG instead of returning a wrong sum).  When all slots are taken an
+ * update folds synchronously (one round trip) instead.
  *
  * These per-call entry points keep drop-in callers (client/lib/client.c,
  * crt/net_pkt.c) working; high-volume hashing belongs in
  * nkfs_xxh64_batch / the fused encode (include/nkfs_gpu.h).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/nkfs_crt.h"
 #include "../../include/nkfs_gpu.h"
 #include "nkfs_internal.h"
 #include "runtime.h"
 
-struct xstate {           /* crt/xxhash.c:515-525 */
+struct xstate {           /* crt/xxhash.c:515-525, + the pending word in the padding */
 	uint64_t total_len;
 	uint64_t seed;
 	uint64_t v[4];
 	uint64_t mem64[4];
 	uint32_t memsize;
+	uint32_t pend;    /* PEND_MAGIC | slot while a message is on the GPU */
 };
 _Static_assert(sizeof(struct xstate) <= sizeof(XXH64_state_t), "XXH64_state_t too small");
 
@@ -43,11 +64,231 @@ static int ensure_gpu(void)
 
 XXH64_state_t *XXH64_createState(void)
 {
-	return crt_malloc(sizeof(XXH64_state_t));
+	XXH64_state_t *st = crt_malloc(sizeof(XXH64_state_t));
+	if (st)
+		memset(st, 0, sizeof(*st));
+	return st;
 }
+
+/* ------------------------------------------------------ message engine */
+
+#define XH_CHUNK (256u << 10) /* staged bytes (whole stripes) per fold launch */
+#define XH_RES 64u            /* pinned result words ahead of the staging */
+
+struct xh {
+	struct nkfs_ctx *c;
+	uint8_t *res;             /* pinned: [digest, flag, v0..v3] */
+	uint64_t *dres;           /* its device-visible address */
+	uint8_t *stage[2];
+	const uint8_t *dstage[2];
+	int cur;
+	int inflight[2];          /* a fold reads stage[b] until ev[b] */
+	uint32_t fill;            /* bytes staged in stage[cur] */
+	int folded;               /* accumulators live on the device */
+	uint64_t *v_dev;
+	uint64_t v0[4];           /* accumulators when the message started */
+};
+
+static int xh_begin(struct xh *h, const uint64_t v[4])
+{
+	memset(h, 0, sizeof(*h));
+	if (ensure_gpu())
+		return -ENODEV;
+	h->c = nkfs_ctx_get();
+	if (!h->c)
+		return -EIO;
+	void *hv, *dv, *dp;
+	int err;
+	if ((err = nkfs_ctx_host(h->c, XH_RES + 2 * XH_CHUNK, &hv)) || (err = nkfs_ctx_dev(h->c, 64, &dv)) ||
+	    (err = nkfs_ctx_events(h->c)))
+		goto fail;
+	if (hipHostGetDevicePointer(&dp, hv, 0) != hipSuccess) {
+		err = -EIO;
+		goto fail;
+	}
+	h->res = hv;
+	h->dres = dp;
+	h->stage[0] = (uint8_t *)hv + XH_RES;
+	h->stage[1] = h->stage[0] + XH_CHUNK;
+	h->dstage[0] = (const uint8_t *)dp + XH_RES;
+	h->dstage[1] = h->dstage[0] + XH_CHUNK;
+	h->v_dev = dv;
+	memcpy(h->v0, v, 32);
+	return 0;
+fail:
+	nkfs_ctx_put(h->c);
+	h->c = NULL;
+	return err;
+}
+
+static void xh_end(struct xh *h)
+{
+	if (h->c) {
+		/* folds still reading the staging finish before the context is reused */
+		for (int b = 0; b < 2; b++)
+			if (h->inflight[b])
+				(void)hipEventSynchronize(h->c->ev[b]);
+		nkfs_ctx_put(h->c);
+	}
+	h->c = NULL;
+}
+
+static void xh_args(const struct xh *h, struct nkfs_xxh_args *a, uint32_t flags)
+{
+	memset(a, 0, sizeof(*a));
+	memcpy(a->v, h->v0, 32);
+	a->src = h->dstage[h->cur];
+	a->nst = h->fill / 32;
+	a->v_dev = h->v_dev;
+	a->out = h->dres;
+	a->flags = flags | (h->folded ? NKFS_XXH_FROM_DEV : 0);
+}
+
+/* fold the staged chunk asynchronously; its buffer is reusable after ev */
+static int xh_flush(struct xh *h)
+{
+	struct nkfs_xxh_args a;
+	xh_args(h, &a, NKFS_XXH_TO_DEV);
+	int err = nkfs_launch_xxh64_chain(&a, h->c->stream);
+	if (err)
+		return err;
+	if (hipEventRecord(h->c->ev[h->cur], h->c->stream) != hipSuccess)
+		return -EIO;
+	h->inflight[h->cur] = 1;
+	h->folded = 1;
+	h->cur ^= 1;
+	h->fill = 0;
+	if (h->inflight[h->cur]) {  /* the fold two chunks back read this buffer */
+		if (hipEventSynchronize(h->c->ev[h->cur]) != hipSuccess)
+			return -EIO;
+		h->inflight[h->cur] = 0;
+	}
+	return 0;
+}
+
+/* stage `bytes` (a multiple of 32) of whole stripes */
+static int xh_stage(struct xh *h, const uint8_t *p, uint64_t bytes)
+{
+	while (bytes) {
+		const uint64_t room = XH_CHUNK - h->fill;
+		const uint64_t take = bytes < room ? bytes : room;
+		memcpy(h->stage[h->cur] + h->fill, p, take);
+		h->fill += (uint32_t)take;
+		p += take;
+		bytes -= take;
+		if (h->fill == XH_CHUNK) {
+			int err = xh_flush(h);
+			if (err)
+				return err;
+		}
+	}
+	return 0;
+}
+
+/* Launch the last fold with `flags` (EMIT / FINISH) and wait for its
+ * completion word: a spin on pinned memory, with the stream's own status
+ * checked now and then so a failed launch cannot spin forever. */
+static int xh_complete(struct xh *h, uint32_t flags, const struct xstate *s, uint64_t *digest, uint64_t v[4])
+{
+	struct nkfs_xxh_args a;
+	xh_args(h, &a, flags);
+	if (s) {
+		a.total_len = s->total_len;
+		a.seed = s->seed;
+		a.tail_len = s->memsize;
+		memcpy(a.tail, s->mem64, s->memsize);
+	}
+	volatile uint64_t *res = (volatile uint64_t *)h->res;
+	a.flag = ++h->c->seq | (1ull << 63);
+	res[1] = 0;
+	int err = nkfs_launch_xxh64_chain(&a, h->c->stream);
+	if (err)
+		return err;
+	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a.flag; spin++) {
+		if ((spin & 0xFFFF) == 0xFFFF) {
+			hipError_t q = hipStreamQuery(h->c->stream);
+			if (q != hipSuccess && q != hipErrorNotReady)
+				return -EIO;
+			if (q == hipSuccess && __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a.flag)
+				return -EIO; /* the stream drained without the word */
+		}
+		__builtin_ia32_pause();
+	}
+	if (digest)
+		*digest = res[0];
+	if (v)
+		for (int i = 0; i < 4; i++)
+			v[i] = res[2 + i];
+	return 0;
+}
+
+/* ------------------------------------------------------- pending slots */
+
+#define NSLOT 1024
+#define PEND_MAGIC 0xC5A10000u
+
+struct xslot {
+	uint64_t token;
+	int used;
+	struct xh h;
+};
+static struct xslot g_slot[NSLOT];
+static pthread_mutex_t g_slot_lock = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t g_token = 0x6E6B38465A5A0001ull;
+
+/* the slot of a pending state, NULL if none; *stale = the state claims one
+ * that is gone (a byte copy of a pending state that was digested) */
+static struct xslot *slot_of(const struct xstate *s, int *stale)
+{
+	*stale = 0;
+	if ((s->pend & 0xFFFF0000u) != PEND_MAGIC)
+		return NULL;
+	const uint32_t i = s->pend & 0xFFFFu;
+	struct xslot *sl = i < NSLOT ? &g_slot[i] : NULL;
+	pthread_mutex_lock(&g_slot_lock);
+	const int ok = sl && sl->used && sl->token == s->v[0];
+	pthread_mutex_unlock(&g_slot_lock);
+	if (!ok) {
+		*stale = 1;
+		return NULL;
+	}
+	return sl;
+}
+
+static struct xslot *slot_take(void)
+{
+	pthread_mutex_lock(&g_slot_lock);
+	for (int i = 0; i < NSLOT; i++)
+		if (!g_slot[i].used) {
+			g_slot[i].used = 1;
+			g_slot[i].token = g_token++;
+			pthread_mutex_unlock(&g_slot_lock);
+			return &g_slot[i];
+		}
+	pthread_mutex_unlock(&g_slot_lock);
+	return NULL;
+}
+
+static void slot_free(struct xslot *sl)
+{
+	xh_end(&sl->h);
+	pthread_mutex_lock(&g_slot_lock);
+	sl->used = 0;
+	sl->token = 0;
+	pthread_mutex_unlock(&g_slot_lock);
+}
+
+/* ------------------------------------------------------------ the ABI */
 
 XXH_errorcode XXH64_freeState(XXH64_state_t *state)
 {
+	if (state) {
+		struct xstate *s = (struct xstate *)state;
+		int stale;
+		struct xslot *sl = slot_of(s, &stale);
+		if (sl)
+			slot_free(sl);
+	}
 	crt_free(state);
 	return XXH_OK;
 }
@@ -55,6 +296,10 @@ XXH_errorcode XXH64_freeState(XXH64_state_t *state)
 XXH_errorcode XXH64_reset(XXH64_state_t *state_in, unsigned long long seed)
 {
 	struct xstate *s = (struct xstate *)state_in;
+	int stale;
+	struct xslot *sl = slot_of(s, &stale);
+	if (sl) /* a message abandoned mid-stream */
+		slot_free(sl);
 	s->seed = seed;
 	s->v[0] = seed + P1 + P2;
 	s->v[1] = seed + P2;
@@ -62,66 +307,8 @@ XXH_errorcode XXH64_reset(XXH64_state_t *state_in, unsigned long long seed)
 	s->v[3] = seed - P1;
 	s->total_len = 0;
 	s->memsize = 0;
+	s->pend = 0;
 	return XXH_OK;
-}
-
-/* Stripes per device pass: the input streams through bounded pinned and
- * device scratch (8 MiB + the state), so any length hashes without a
- * device allocation of its size. */
-#define FOLD_CHUNK (8u << 20)
-
-/* Fold the buffered stripe (if `lead`) and `nst_input` stripes of the
- * caller's bytes into s->v on the device: state + stripes are staged in
- * pinned memory and go over in one copy per chunk; the accumulators stay
- * on the device between chunks and come back once. */
-static int fold_stripes(struct xstate *s, const uint8_t *lead, const uint8_t *input, uint64_t nst_input)
-{
-	struct nkfs_ctx *c = nkfs_ctx_get();
-	if (!c)
-		return -EIO;
-	int err;
-	const uint64_t total = (lead ? 1 : 0) + nst_input;  /* stripes */
-	const uint64_t first = total * 32 < FOLD_CHUNK ? total * 32 : FOLD_CHUNK;
-	void *dv, *hv;
-	if ((err = nkfs_ctx_dev(c, 64 + first, &dv)) || (err = nkfs_ctx_host(c, 64 + first, &hv)))
-		goto out;
-	uint8_t *d = dv, *h = hv;
-	memcpy(h, s->v, 32);
-	uint64_t done = 0;  /* input stripes consumed */
-	for (int pass = 0; done < nst_input || (pass == 0 && lead); pass++) {
-		uint64_t off = pass == 0 ? 32 : 0; /* pass 0 carries the state */
-		uint64_t room = (FOLD_CHUNK - (pass == 0 && lead ? 32 : 0)) / 32;
-		uint64_t take = nst_input - done < room ? nst_input - done : room;
-		uint8_t *hp = h + 32;
-		if (pass == 0 && lead) {
-			memcpy(hp, lead, 32);
-			hp += 32;
-		}
-		if (pass) /* the previous pass's copy must be done before the staging is reused */
-			if (hipStreamSynchronize(c->stream) != hipSuccess) {
-				err = -EIO;
-				goto out;
-			}
-		memcpy(hp, input + done * 32, take * 32);
-		const uint64_t nst = take + (pass == 0 && lead ? 1 : 0);
-		if (hipMemcpyAsync(d + 32 - off, h + 32 - off, off + nst * 32, hipMemcpyHostToDevice, c->stream) !=
-		    hipSuccess) {
-			err = -EIO;
-			goto out;
-		}
-		if ((err = nkfs_launch_xxh64_stripes((uint64_t *)d, d + 32, nst, c->stream)))
-			goto out;
-		done += take;
-	}
-	if (hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-	    hipStreamSynchronize(c->stream) != hipSuccess) {
-		err = -EIO;
-		goto out;
-	}
-	memcpy(s->v, h, 32);
-out:
-	nkfs_ctx_put(c);
-	return err;
 }
 
 XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t len)
@@ -137,22 +324,53 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 		s->total_len += len;
 		return XXH_OK;
 	}
-	if (ensure_gpu())
+	int stale;
+	struct xslot *sl = slot_of(s, &stale);
+	if (stale)
 		return XXH_ERROR;
-	const uint8_t *lead = NULL;
+	struct xh local, *h;
+	if (sl) {
+		h = &sl->h;
+	} else {
+		sl = slot_take();
+		h = sl ? &sl->h : &local; /* no slot free: fold synchronously */
+		if (xh_begin(h, s->v)) {
+			if (sl)
+				slot_free(sl);
+			return XXH_ERROR;
+		}
+		if (sl) {
+			s->v[0] = sl->token;
+			s->pend = PEND_MAGIC | (uint32_t)(sl - g_slot);
+		}
+	}
+	int err = 0;
 	if (s->memsize) {
-		size_t fill = 32 - s->memsize;
+		const size_t fill = 32 - s->memsize;
 		memcpy((uint8_t *)s->mem64 + s->memsize, p, fill);
 		p += fill;
 		len -= fill;
 		s->total_len += fill;
-		lead = (const uint8_t *)s->mem64;
 		s->memsize = 0;
+		err = xh_stage(h, (const uint8_t *)s->mem64, 32);
 	}
-	uint64_t nst = len / 32;
-	if (lead || nst) {
-		if (fold_stripes(s, lead, p, nst))
-			return XXH_ERROR;
+	const uint64_t nst = len / 32;
+	if (!err && nst)
+		err = xh_stage(h, p, nst * 32);
+	if (!err && h == &local) {
+		uint64_t v[4];
+		err = xh_complete(h, NKFS_XXH_EMIT, NULL, NULL, v);
+		if (!err)
+			memcpy(s->v, v, 32);
+	}
+	if (h == &local)
+		xh_end(h);
+	if (err) {
+		if (h != &local) {
+			slot_free(sl);
+			s->pend = 0;
+		}
+		return XXH_ERROR;
 	}
 	p += nst * 32;
 	len -= nst * 32;
@@ -164,45 +382,39 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 }
 
 /* returns 0 and fills *out, or a negative errno */
-static int finish(const struct xstate *s, uint64_t *out)
+static int finish(struct xstate *s, uint64_t *out)
 {
-	if (ensure_gpu())
-		return -ENODEV;
-	struct nkfs_ctx *c = nkfs_ctx_get();
-	if (!c)
-		return -EIO;
-	int err;
-	void *dv, *hv;
-	if ((err = nkfs_ctx_dev(c, 80, &dv)) || (err = nkfs_ctx_host(c, 80, &hv)))
-		goto out;
-	uint8_t *d = dv, *h = hv;
-	memcpy(h, s->v, 32);
-	memcpy(h + 32, s->mem64, 32);
-	if (hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-		err = -EIO;
-		goto out;
+	int stale;
+	struct xslot *sl = slot_of(s, &stale);
+	if (stale)
+		return -EINVAL;
+	if (!sl) { /* nothing on the GPU: merge + tail + avalanche in one launch */
+		struct xh h;
+		int err = xh_begin(&h, s->v);
+		if (!err)
+			err = xh_complete(&h, NKFS_XXH_FINISH, s, out, NULL);
+		xh_end(&h);
+		return err;
 	}
-	if ((err = nkfs_launch_xxh64_finish((uint64_t *)(d + 64), (const uint64_t *)d, s->total_len, s->seed, d + 32,
-					    s->memsize, c->stream)))
-		goto out;
-	if (hipMemcpyAsync(h + 64, d + 64, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-	    hipStreamSynchronize(c->stream) != hipSuccess) {
-		err = -EIO;
-		goto out;
-	}
-	memcpy(out, h + 64, 8);
-out:
-	nkfs_ctx_put(c);
-	return err;
+	uint64_t v[4];
+	int err = xh_complete(&sl->h, NKFS_XXH_FINISH | NKFS_XXH_EMIT, s, out, v);
+	slot_free(sl);
+	s->pend = 0;
+	if (err)
+		return err;
+	/* the state is now what the reference's is after the same updates */
+	memcpy(s->v, v, 32);
+	return 0;
 }
 
 /* The reference returns a digest unconditionally; a GPU failure here has
  * no error channel, so it traps like CRT_BUG rather than return a wrong
- * checksum. */
+ * checksum.  The accumulators of a pending message are written back into
+ * the caller's state (it was writable: XXH64_update wrote it). */
 unsigned long long XXH64_digest(const XXH64_state_t *state_in)
 {
 	uint64_t h;
-	if (finish((const struct xstate *)state_in, &h))
+	if (finish((struct xstate *)state_in, &h))
 		__builtin_trap();
 	return h;
 }
@@ -210,6 +422,7 @@ unsigned long long XXH64_digest(const XXH64_state_t *state_in)
 unsigned long long XXH64(const void *input, size_t length, unsigned long long seed)
 {
 	XXH64_state_t st;
+	memset(&st, 0, sizeof(st));
 	XXH64_reset(&st, seed);
 	if (XXH64_update(&st, input, length) != XXH_OK)
 		__builtin_trap();

@@ -1,0 +1,374 @@
+// nk8_big.hip -- encode and decode for k > 16.  The reference accepts any
+// 2 <= k <= n <= 255 with k <= 254 (crt/nk8.c:13-16, 356-360, 463-467), and
+// its own load-time self test draws k uniform in [2, 254] (crt/nk8.c:735-744).
+//
+// Reference arithmetic: crt/nk8.c:403-420 -- part_i[j] = XOR_m x_i^m d[j*k+m]
+// (d zero past block_size, :393-398); crt/nk8.c:552-582 -- block[j*k+m] =
+// XOR_c part_c[j] W[c][m], W the inverse of the survivors' Vandermonde rows
+// (k_decode_prep leaves the first k distinct survivors and W in `work`).
+//
+// Both directions are a per-stripe GF(2^8) matrix apply, k inputs -> n (or k)
+// outputs per row.  With k > 16 the packed product tables of every input
+// column no longer fit in LDS, so the inputs are taken 16 columns at a time:
+// table j of a column chunk, U_j[x] = (M[j][o0] x, ..., M[j][o0+15] x),
+// gives one row's term for 16 outputs per ds_read_b128, and a lane XORs the
+// 16 terms of its row into a 16-byte accumulator that lives across chunks.
+// Tables are rebuilt per chunk (64 KiB, four per wave by Gray-code walk) and
+// amortised over a slice of thousands of rows.  Lane = row for the strided
+// side (interleaved rows of k bytes: encode reads them, decode writes them),
+// so one wave instruction covers 64 consecutive rows.
+//
+//  k_encode_big  workgroup = (stripe, group of 16 parts, slice of 4,096 rows);
+//                a lane's row bytes come from dword-aligned 16+4-byte loads
+//                and v_alignbyte (k is arbitrary); a slice's 16 x 256-row
+//                outputs go through an LDS [part quad][row] stage and a 4x4
+//                byte transpose, so each store instruction writes 256
+//                contiguous bytes of one part.  The groups of a (stripe,
+//                slice) are dispatched back to back on one XCD (workgroup b
+//                runs on XCD b mod 8) and share the block's lines in its L2.
+//  k_decode_big  workgroup = (stripe, group of 16 output columns, slice of
+//                1,024 rows); a chunk's survivor bytes by byte loads (64
+//                consecutive bytes of one part per wave instruction) into an
+//                LDS row stage; a lane writes its row's 16 columns, and the
+//                groups of a (stripe, slice) run back to back on one XCD so
+//                the rows' lines complete in its L2.
+// XXH64 of the parts is the batched message hash afterwards (a part's chain
+// is serial over all of its rows, and a stripe's rows are spread over slices).
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+
+#include "nk8_dev.h"
+
+using namespace nkfs;
+using namespace nkfs::dev;
+
+namespace {
+
+
+
+
+constexpr int ENC_T = 16;                    // rows per lane per encode slice
+constexpr u32 ENC_ROWS = 256u * ENC_T;       // rows per encode workgroup
+
+__device__ inline __amdgpu_buffer_rsrc_t brsrc(const void *base, u32 bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+
+// x^e over GF(2^8) for x != 0 by the log/antilog tables (x^0 = 1)
+__device__ inline u32 gf_pow(const GfTables *t, u32 x, u32 e)
+{
+    if (!x)
+        return e ? 0u : 1u;
+    return t->exp[(u32(t->log[x]) * e) % 255u];
+}
+
+__global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *ids, const GfTables *gft,
+                                                       u32 ngroups, u32 nslices)
+{
+    __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];   // 16 tables of 256 x 16 B
+    __shared__ __attribute__((aligned(16))) u32 stage[4 * 256];      // [part quad][row]
+    __shared__ __attribute__((aligned(16))) uint4 coef[256];         // coef[m] = (x_{p0+e}^m), e < 16
+
+    const u32 b = blockIdx.x;
+    const u32 loc = b >> 3;
+    const u32 grp = loc % ngroups;
+    const u32 slice = (loc / ngroups) % nslices;
+    const u32 s = (loc / ngroups / nslices) * 8 + (b & 7);
+    if (s >= g.nstripes)
+        return;  // the whole workgroup: no barrier is skipped by part of it
+    const Stripe v = stripe_at(g, s);
+    const u32 r_begin = slice * ENC_ROWS;
+    if (r_begin >= v.ps)
+        return;
+    const int n = g.n, k = g.k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int p0 = int(grp) * 16, np = min(16, n - p0);
+
+    // Vandermonde rows of the group's parts: coef[m] byte e = x_{p0+e}^m
+    // (crt/nk8.c:404-406 builds the same powers by repeated multiplication)
+    {
+        const u8 *sid = ids + u64(s) * u64(n) + p0;
+        for (int m = tid; m < k; m += 256) {
+            u32 w[4] = {0, 0, 0, 0};
+            for (int e = 0; e < np; ++e)
+                w[e >> 2] |= gf_pow(gft, sid[e], u32(m)) << (8 * (e & 3));
+            coef[m] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+
+    // the stripe's block through a buffer resource based at the dword below
+    // it: loads are dword aligned and anything past B reads 0 (the tail
+    // bytes inside the last dword are masked below)
+    const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
+    const __amdgpu_buffer_rsrc_t rs = brsrc(v.blk - mis, (v.B + mis + 3u) & ~3u);
+
+    uint4 acc[ENC_T];
+#pragma unroll
+    for (int t = 0; t < ENC_T; ++t)
+        acc[t] = make_uint4(0, 0, 0, 0);
+
+    const int nch = (k + 15) / 16;
+    for (int cc = 0; cc < nch; ++cc) {
+        __syncthreads();  // coef[] written / the previous chunk's lookups done
+        // wave w builds tables j = w, w+4, w+8, w+12 of columns 16cc + j
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+            const int j = wave + 4 * q, m = 16 * cc + j;
+            const uint4 c = m < k ? coef[m] : make_uint4(0, 0, 0, 0);  // columns past k: zero table
+            const u32 row[4] = {c.x, c.y, c.z, c.w};
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            build_table16(tbl + j * 4096, basis, lane);
+        }
+        __syncthreads();
+        // tdep (0 at run time) chains each row's lookups and the next row's
+        // loads behind the previous row's XORs: unchained, the compiler
+        // hoists all 16 rows' loads and 256 lookups and spills
+        u32 tdep = 0;
+        auto load = [&](int t, v4u &x, u32 &x4, u32 &pos) {
+            const u32 r = r_begin + u32(t) * 256u + u32(tid);
+            pos = r * u32(k) + 16u * u32(cc);  // block byte of column 16cc of row r
+            const u32 a = (pos + mis + tdep) & ~3u;
+            x = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+            x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
+        };
+        v4u xc, xn;
+        u32 x4c, x4n, posc, posn;
+        load(0, xc, x4c, posc);
+#pragma unroll
+        for (int t = 0; t < ENC_T; ++t) {
+            if (t + 1 < ENC_T)
+                load(t + 1, xn, x4n, posn);
+            const u32 sh = (posc + mis) & 3u;
+            u32 d[4];
+            d[0] = __builtin_amdgcn_alignbyte(xc.y, xc.x, sh);
+            d[1] = __builtin_amdgcn_alignbyte(xc.z, xc.y, sh);
+            d[2] = __builtin_amdgcn_alignbyte(xc.w, xc.z, sh);
+            d[3] = __builtin_amdgcn_alignbyte(x4c, xc.w, sh);
+            // bytes at or past B are zero (the reference zero-pads its tail
+            // row, crt/nk8.c:393-398); columns past k meet zero tables
+            {
+                // branch-free: a branch here splits the step's block
+                const u32 valid = v.B > posc ? min(v.B - posc, 16u) : 0u;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
+                    d[w] &= u32((u64(1) << (8 * keep)) - 1u);
+                }
+            }
+            uint4 e = acc[t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const u32 byte = (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
+                e.x ^= tv.x;
+                e.y ^= tv.y;
+                e.z ^= tv.z;
+                e.w ^= tv.w;
+            }
+            acc[t] = e;
+            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+            xc = xn;
+            x4c = x4n;
+            posc = posn;
+        }
+    }
+
+    // 256 rows x 16 parts per t-unit: [part quad][row] in LDS (conflict-free
+    // dword writes), read back as 4 rows x 4 parts (ds_read_b128), 4x4 byte
+    // transpose, one dword of 4 rows per part: wave w stores parts
+    // 4w..4w+3, 64 lanes x 4 B = 256 contiguous bytes per instruction
+    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
+#pragma unroll
+    for (int t = 0; t < ENC_T; ++t) {
+        const u32 rt = r_begin + u32(t) * 256u;
+        if (rt >= v.ps)
+            break;  // workgroup-uniform
+        __syncthreads();
+        stage[0 * 256 + tid] = acc[t].x;
+        stage[1 * 256 + tid] = acc[t].y;
+        stage[2 * 256 + tid] = acc[t].z;
+        stage[3 * 256 + tid] = acc[t].w;
+        __syncthreads();
+        const uint4 q4 = *reinterpret_cast<const uint4 *>(stage + wave * 256 + 4 * lane);
+        u32 o[4];
+        transpose4(q4.x, q4.y, q4.z, q4.w, o[0], o[1], o[2], o[3]);
+        const u32 rr = rt + 4u * u32(lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * wave + j;
+            if (e < np && rr < v.ps) {
+                u8 *dst = v.parts + u64(p0 + e) * v.pitch + rr;
+                if (pal && rr + 4u <= v.ps) {
+                    *reinterpret_cast<u32 *>(dst) = o[j];
+                } else {
+                    for (u32 c = 0; c < 4 && rr + c < v.ps; ++c)
+                        dst[c] = u8(o[j] >> (8 * c));
+                }
+            }
+        }
+    }
+}
+
+// Decode: one workgroup per (stripe, group of 16 output columns, slice of
+// 256*DEC_T rows).
+constexpr int DEC_T = 4;  // 64 KiB tables + 16 KiB row stage: two workgroups per CU
+constexpr u32 DEC_ROWS = 256u * DEC_T;
+
+__global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *work, const int32_t *status,
+                                                       u32 ngroups, u32 nslices)
+{
+    __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];
+    __shared__ __attribute__((aligned(16))) uint4 ins[DEC_T][256];  // a chunk's survivor bytes per row
+    const u32 b = blockIdx.x;
+    const u32 loc = b >> 3;
+    const u32 h = loc % ngroups;
+    const u32 slice = (loc / ngroups) % nslices;
+    const u32 s = (loc / ngroups / nslices) * 8 + (b & 7);
+    if (s >= g.nstripes || (status && status[s]))
+        return;
+    const Stripe v = stripe_at(g, s);  // g.blocks = the output, g.n = slots per stripe
+    const u32 r_begin = slice * DEC_ROWS;
+    if (r_begin >= v.ps)
+        return;
+    const int k = g.k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const u8 *wk = work + u64(s) * u64(k + k * k);
+
+    uint4 acc[DEC_T];
+#pragma unroll
+    for (int t = 0; t < DEC_T; ++t)
+        acc[t] = make_uint4(0, 0, 0, 0);
+
+    const int nch = (k + 15) / 16;
+    for (int cc = 0; cc < nch; ++cc) {
+        __syncthreads();  // the previous chunk's tables and rows are consumed
+        // survivor bytes of columns 16cc.. of my rows (one row per lane per
+        // t; a wave instruction reads 64 consecutive bytes of one part),
+        // packed into the LDS row stage
+#pragma unroll 1
+        for (int t = 0; t < DEC_T; ++t) {
+            const u32 r = r_begin + u32(t) * 256u + u32(tid);
+            u32 w[4] = {0, 0, 0, 0};
+            if (r < v.ps)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int c = 16 * cc + j;
+                    if (c < k)
+                        w[j >> 2] |= u32(v.parts[u64(wk[c]) * v.pitch + r]) << (8 * (j & 3));
+                }
+            ins[t][tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        // table j: survivor 16cc+j, U_j[x] = (W[c][16h] x, ..., W[c][16h+15] x)
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+            const int j = wave + 4 * q, c = 16 * cc + j;
+            u32 row[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = 16 * int(h) + e;
+                if (c < k && m < k)
+                    row[e >> 2] |= u32(wk[k + c * k + m]) << (8 * (e & 3));
+            }
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            build_table16(tbl + j * 4096, basis, lane);
+        }
+        __syncthreads();
+        u32 tdep = 0;  // 0 at run time: one row's lookups in flight at a time
+#pragma unroll
+        for (int t = 0; t < DEC_T; ++t) {
+            const uint4 iv = ins[t][tid];
+            const u32 in[4] = {iv.x, iv.y, iv.z, iv.w};
+            uint4 e = acc[t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const u32 byte = (in[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
+                e.x ^= tv.x;
+                e.y ^= tv.y;
+                e.z ^= tv.z;
+                e.w ^= tv.w;
+            }
+            acc[t] = e;
+            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+        }
+    }
+
+    // row r's bytes 16h..16h+15 at r*k + 16h (fewer in the last group;
+    // nothing at or past B); the other groups' workgroups of this slice run
+    // on the same XCD, so the lines complete in its L2
+    u8 *out = const_cast<u8 *>(v.blk);
+    const uintptr_t oa = reinterpret_cast<uintptr_t>(out);
+#pragma unroll
+    for (int t = 0; t < DEC_T; ++t) {
+        const u32 r = r_begin + u32(t) * 256u + u32(tid);
+        if (r >= v.ps)
+            continue;
+        const u64 rb = u64(r) * u64(k);
+        const u64 off = rb + 16u * h;
+        const u32 tw[4] = {acc[t].x, acc[t].y, acc[t].z, acc[t].w};
+        const u64 lim = min(u64(v.B), rb + u64(k));  // this row's bytes
+        if (off + 16 <= lim && ((oa + off) & 15) == 0) {
+            store16(out + off, tw[0], tw[1], tw[2], tw[3], false);
+        } else if (off + 16 <= lim && ((oa + off) & 3) == 0) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                *reinterpret_cast<u32 *>(out + off + 4 * w) = tw[w];
+        } else {
+#pragma unroll
+            for (u32 c = 0; c < 16; ++c)
+                if (off + c < lim)
+                    out[off + c] = u8(tw[c >> 2] >> (8 * (c & 3)));
+        }
+    }
+}
+
+}  // namespace
+
+// Encode (no hash) a uniform or ragged batch with any 2 <= k <= 254, n <= 255
+// through 16-column chunks.  -ENOSYS where a stripe's buffer offsets would
+// not fit 31 bits.
+extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const void *gf, hipStream_t st)
+{
+    const int k = g->k;
+    if (k < 2 || k > 254 || g->n < k || g->n > 255)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    if (u64(g->block_size) + 64u > 0x7FFFFFFFull)
+        return -ENOSYS;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 ngroups = (u64(g->n) + 15) / 16;
+    const u64 nslices = (u64(ps_max) + ENC_ROWS - 1) / ENC_ROWS;
+    const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
+    if (grid > 0x7FFFFFFFull)
+        return -EINVAL;
+    hipLaunchKernelGGL(k_encode_big, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
+                       u32(ngroups), u32(nslices ? nslices : 1));
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// Decode a uniform or ragged batch with 2 <= k <= 254 from the plan
+// k_decode_prep left in `work` (stripes with status != 0 are skipped).
+extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st)
+{
+    const int k = g->k;
+    if (k < 2 || k > 254)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    if (u64(g->block_size) + 64u > 0x7FFFFFFFull)
+        return -ENOSYS;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 ngroups = (u64(k) + 15) / 16;
+    const u64 nslices = (u64(ps_max) + DEC_ROWS - 1) / DEC_ROWS;
+    const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
+    if (grid > 0x7FFFFFFFull)
+        return -EINVAL;
+    hipLaunchKernelGGL(k_decode_big, dim3(u32(grid)), dim3(256), 0, st, *g, work, status, u32(ngroups),
+                       u32(nslices ? nslices : 1));
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

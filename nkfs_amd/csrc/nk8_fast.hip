@@ -315,7 +315,7 @@ static int launch_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
 {
     constexpr int G = E == 4 ? 4 : 2;
     const dim3 grid((g.nstripes + G - 1) / G);
-    const int cap = nkfs_g_tune.enc_fused_waves_per_cu;
+    const int cap = nkfs_tune_now().enc_fused_waves_per_cu;
     switch (k) {
 #define NKFS_K(KK)                                                                                      \
     case KK:                                                                                            \
@@ -793,7 +793,7 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     while (!verify && groups * slices < target && steps / (slices * 2) >= 4)
         slices *= 2;
     const dim3 grid(groups * slices);
-    const int cap = nkfs_g_tune.dec_wave_waves_per_cu;
+    const int cap = nkfs_tune_now().dec_wave_waves_per_cu;
 #define NKFS_DK(KK, EE, GG)                                                                                       \
     do {                                                                                                          \
         if (verify)                                                                                               \

@@ -563,7 +563,7 @@ extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
 template <class F>
 static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 {
-    if (!g->block_sizes || g->order || !nkfs_g_tune.size_order)
+    if (!g->block_sizes || g->order || !nkfs_tune_now().size_order)
         return -ENOSYS;
     u32 *perm = nullptr;
     if (hipMallocAsync(reinterpret_cast<void **>(&perm), size_t(g->nstripes) * sizeof(u32), st) != hipSuccess)
@@ -581,6 +581,8 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,
                                 int cus, hipStream_t st);
 extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st);
+extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const void *gf, hipStream_t st);
+extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
@@ -607,7 +609,7 @@ static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
 
 static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStream_t st)
 {
-    const nkfs_tune &t = nkfs_g_tune;
+    const nkfs_tune t = nkfs_tune_now();
     const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
                      : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
                                                                   : NKFS_ENC_AUTO;
@@ -631,7 +633,7 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
 static bool few_big_stripes(const nkfs_geom *g)
 {
     const u32 ps = max_part_size(g, g->block_size);
-    return !g->block_sizes && nkfs_g_tune.enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
+    return !g->block_sizes && nkfs_tune_now().enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
            g->nstripes < 64 && ps >= 8192;
 }
 
@@ -642,18 +644,21 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         return 0;
     hipStream_t st = (hipStream_t)stream;
     int rc = -ENOSYS;
-    const int kern = nkfs_g_tune.enc_kernel;
-    if (g->n <= 8 && g->k <= 8 && kern != NKFS_ENC_GENERIC && kern != NKFS_ENC_WIDE && !few_big_stripes(g)) {
+    const int kern = nkfs_tune_now().enc_kernel;
+    if (g->n <= 8 && g->k <= 8 && kern != NKFS_ENC_GENERIC && kern != NKFS_ENC_WIDE && kern != NKFS_ENC_BIG &&
+        !few_big_stripes(g)) {
         rc = with_size_order(g, st, [&](const nkfs_geom *go) { return fast_encode(go, ids, digests, st); });
         if (rc == -ENOSYS)
             rc = fast_encode(g, ids, digests, st);
     }
     if (rc != -ENOSYS)
         return rc;
-    // n > 8 (or a few big stripes): part groups of 8 for k <= 16, then the
-    // batched XXH64 of the parts
+    // n > 8 (or a few big stripes): part groups of 8 for k <= 16, 16-column
+    // chunks beyond (nk8_big.hip), then the batched XXH64 of the parts
     if (kern != NKFS_ENC_GENERIC) {
-        rc = nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
+        rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
+        if (rc == -ENOSYS)
+            rc = nkfs_big_encode(g, ids, gf, st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
     }
@@ -669,7 +674,7 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
 
 extern "C" int nkfs_launch_hash_parts(const nkfs_geom *g, uint64_t *digests, void *stream)
 {
-    if (nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC)
+    if (nkfs_tune_now().enc_kernel != NKFS_ENC_GENERIC)
         return nkfs_fast_xxh64_parts(g, digests, (hipStream_t)stream);
     const u64 threads = u64(g->nstripes) * u64(g->n) * 4;
     if (!threads)
@@ -686,9 +691,9 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     if (!g->nstripes)
         return 0;
     hipStream_t st = (hipStream_t)stream;
-    const nkfs_tune &t = nkfs_g_tune;
+    const nkfs_tune t = nkfs_tune_now();
     int rc = -ENOSYS;
-    if (g->k <= 8 && t.dec_kernel != NKFS_DEC_GENERIC && t.dec_kernel != NKFS_DEC_WIDE) {
+    if (g->k <= 8 && t.dec_kernel != NKFS_DEC_GENERIC && t.dec_kernel != NKFS_DEC_WIDE && t.dec_kernel != NKFS_DEC_BIG) {
         // uniform batches without the integrity check: one-shot slice waves;
         // ragged batches and the verifying form: the wave-per-stripe decoder
         // default: one-shot slices for k >= 3 (C3/C4 decode +10-15 %); for
@@ -719,10 +724,13 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     rc = launch_ok();
     if (rc)
         return rc;
-    // k <= 16: survivor tables of 16-byte products (nk8_wide.hip); beyond,
-    // or pinned: thread per row
-    rc = t.dec_kernel != NKFS_DEC_GENERIC ? nkfs_wide_decode(g, (const u8 *)work, status, nkfs_cu_count(), st)
-                                          : -ENOSYS;
+    // k <= 16: survivor tables of 16-byte products (nk8_wide.hip); beyond:
+    // 16-column chunks (nk8_big.hip); pinned GENERIC: thread per row
+    rc = t.dec_kernel == NKFS_DEC_GENERIC || t.dec_kernel == NKFS_DEC_BIG
+             ? -ENOSYS
+             : nkfs_wide_decode(g, (const u8 *)work, status, nkfs_cu_count(), st);
+    if (rc == -ENOSYS && t.dec_kernel != NKFS_DEC_GENERIC)
+        rc = nkfs_big_decode(g, (const u8 *)work, status, st);
     if (rc == -ENOSYS) {
         const u32 ps = part_size_of(g->block_size, g->k);
         dim3 grid(g->nstripes, row_blocks(ps));
@@ -756,7 +764,7 @@ extern "C" int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 {
     if (!count)
         return 0;
-    if (nkfs_g_tune.enc_kernel != NKFS_ENC_GENERIC)
+    if (nkfs_tune_now().enc_kernel != NKFS_ENC_GENERIC)
         return nkfs_fast_xxh64_list(base, off, len, count, seed, out, (hipStream_t)stream);
     const u64 threads = u64(count) * 4;
     hipLaunchKernelGGL(k_xxh64_batch, dim3(u32((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, base,

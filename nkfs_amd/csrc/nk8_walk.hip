@@ -127,6 +127,19 @@ __device__ inline void load_rows(u32 (&d)[4 * K], const Stripe &v, u64 off, bool
 
 }  // namespace
 
+// The walk encoder's buffer offsets (block bytes plus a chunk's reach, a
+// stripe's part span, the digest array) all below 2^31 (host-side check;
+// tests/test_abi.py exercises the bound through nkfs_walk_offsets_fit)
+__host__ __device__ inline bool walk_offsets_fit(u64 block_size, u64 part_span, u64 nstripes, u64 n)
+{
+    return block_size + 2048u * 8u <= 0x7FFFFFFFull && part_span <= 0x7FFFFFFFull && nstripes * n * 8u <= 0x7FFFFFFFull;
+}
+
+extern "C" int nkfs_walk_offsets_fit(uint64_t block_size, uint64_t part_span, uint64_t nstripes, uint64_t n)
+{
+    return walk_offsets_fit(block_size, part_span, nstripes, n);
+}
+
 // Buffer offset `off` (< 2^31) when `live`, else past every num_records
 // (the load reads 0 / the store is dropped), as plain
 // arithmetic: a select here tempts the compiler to branch around each
@@ -858,7 +871,7 @@ template <int E, int U, bool HASH, bool NIB>
 static int launch_walk_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
 {
     if constexpr (!NIB)
-        if (nkfs_g_tune.enc_prefetch >= 2)
+        if (nkfs_tune_now().enc_prefetch >= 2)
             return launch_walk_kp<E, U, 2, HASH, NIB>(k, st, g, ids, dig, waves, cus);
     return launch_walk_kp<E, U, 1, HASH, NIB>(k, st, g, ids, dig, waves, cus);
 }
@@ -875,8 +888,9 @@ extern "C" int nkfs_walk_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         return 0;
     const u64 ps = part_size_of_host(g->block_size, g->k);
     const u64 pitch = g->block_sizes ? ((ps + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1)) : g->part_pitch;
-    if (u64(g->block_size) + 2048u * 8u > 0x7FFFFFFFull || u64(g->n) * pitch > 0x7FFFFFFFull ||
-        u64(g->nstripes) * u64(g->n) * 8u > 0xFFFFFFFFull)
+    // every buffer offset must fit 31 bits: live_off() drops a store by
+    // setting bit 31, which lands past num_records only for offsets below 2^31
+    if (!walk_offsets_fit(g->block_size, u64(g->n) * pitch, g->nstripes, g->n))
         return -ENOSYS;
     const bool h = digests != nullptr;
     int rc;

@@ -166,32 +166,6 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
     }
 }
 
-// Packed 16-byte table T[x] = XOR_{bit b of x} basis[b] for one 64-lane wave
-// (lane li owns x = li + 64 j, Gray-code order: one XOR per entry and word).
-__device__ inline void build_table16(u8 *t, const u32 (&basis)[8][4], int li)
-{
-    u32 hv[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        u32 e = 0;
-#pragma unroll
-        for (int b = 0; b < 6; ++b)
-            e ^= basis[b][w] & (0u - ((u32(li) >> b) & 1u));
-        hv[w] = e;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (j) {
-            const int bit = __builtin_ctz(j);
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-                hv[w] ^= basis[6 + bit][w];
-        }
-        const int x = li + 64 * (j ^ (j >> 1));
-        *reinterpret_cast<uint4 *>(t + x * 16) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-    }
-}
-
 // Decode, 2 <= k <= 16: one workgroup (4 waves) per (stripe, row slice).
 // Survivor c's table U_c[x] = (W[c][0] x, ..., W[c][15] x) packs the
 // products for all k output bytes of a row, so a row costs k ds_read_b128 +

@@ -41,7 +41,6 @@ struct nkfs_geom {
 /* Kernel choice and launch shape (struct nkfs_tune, include/nkfs_gpu.h):
  * one process-wide copy, set at init, read by the launchers. */
 struct nkfs_tune;
-extern struct nkfs_tune nkfs_g_tune;
 
 /* Launchers: return 0 or a negative errno; `stream` is a hipStream_t. */
 int nkfs_launch_gf_init(void *gf_tables, void *stream);
@@ -59,6 +58,28 @@ int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v,
 			     uint64_t total_len, uint64_t seed,
 			     const uint8_t *tail, uint32_t tail_len,
 			     void *stream);
+/* One message's XXH64 chains in one wave (xxh64_chain.hip): fold `nst`
+ * 32-byte stripes at `src` (a device-visible pointer: pinned host memory or
+ * device memory) into the accumulators -- from v[] or, with FROM_DEV, from
+ * v_dev[] -- then with TO_DEV store them to v_dev[], with EMIT store them
+ * to out[2..5], with FINISH merge, add total_len, fold the tail (tail_len <
+ * 32 bytes, by value), avalanche and store out[0] = digest; after EMIT or
+ * FINISH out[1] = flag (system-scope release: the host spins on it). */
+enum { NKFS_XXH_FROM_DEV = 1, NKFS_XXH_TO_DEV = 2, NKFS_XXH_FINISH = 4, NKFS_XXH_EMIT = 8 };
+struct nkfs_xxh_args {
+	uint64_t v[4];
+	uint64_t total_len;
+	uint64_t seed;
+	uint64_t nst;
+	const uint8_t *src;
+	uint64_t *v_dev;
+	uint64_t *out;
+	uint64_t flag;
+	uint8_t tail[32];
+	uint32_t tail_len;
+	uint32_t flags;
+};
+int nkfs_launch_xxh64_chain(const struct nkfs_xxh_args *a, void *stream);
 int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 			    const uint64_t *len, uint32_t count, uint64_t seed,
 			    uint64_t *out, void *stream);
@@ -90,4 +111,17 @@ size_t nkfs_gf_tables_bytes(void);
 #ifdef __cplusplus
 }
 #endif
+#ifdef __cplusplus
+#include "../../include/nkfs_gpu.h"
+/* One consistent copy of the process-wide struct nkfs_tune: nkfs_tune_get
+ * copies it under its lock, so a concurrent nkfs_tune_set never tears a
+ * launch's read (the launchers take one copy per decision). */
+static inline nkfs_tune nkfs_tune_now()
+{
+	nkfs_tune t;
+	nkfs_tune_get(&t);
+	return t;
+}
+#endif
+
 #endif

@@ -43,8 +43,11 @@ static struct nkfs_dev g_dev[NKFS_MAX_DEVICES];
 static int g_lanes[NKFS_MAX_DEVICES];
 static int g_nlanes;
 
-/* Measured defaults; nkfs_tune_set replaces them. */
-struct nkfs_tune nkfs_g_tune = {
+/* Measured defaults; nkfs_tune_set replaces them.  Read
+ * and written only under g_tune_lock: every launch takes one consistent
+ * copy (nkfs_tune_now), so a concurrent nkfs_tune_set never tears a read. */
+static pthread_mutex_t g_tune_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct nkfs_tune g_tune = {
 	.enc_kernel = NKFS_ENC_AUTO,
 	.dec_kernel = NKFS_DEC_AUTO,
 	.enc_waves_per_cu = 8,
@@ -60,14 +63,17 @@ struct nkfs_tune nkfs_g_tune = {
 
 void nkfs_tune_get(struct nkfs_tune *t)
 {
-	if (t)
-		*t = nkfs_g_tune;
+	if (!t)
+		return;
+	pthread_mutex_lock(&g_tune_lock);
+	*t = g_tune;
+	pthread_mutex_unlock(&g_tune_lock);
 }
 
 int nkfs_tune_set(const struct nkfs_tune *t)
 {
-	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WIDE || t->dec_kernel < NKFS_DEC_AUTO ||
-	    t->dec_kernel > NKFS_DEC_WIDE || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
+	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_BIG || t->dec_kernel < NKFS_DEC_AUTO ||
+	    t->dec_kernel > NKFS_DEC_BIG || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||
@@ -75,7 +81,9 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->enc_fused_waves_per_cu && (t->enc_fused_waves_per_cu < 3 || t->enc_fused_waves_per_cu > 32)) ||
 	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)))
 		return -EINVAL;
-	nkfs_g_tune = *t;
+	pthread_mutex_lock(&g_tune_lock);
+	g_tune = *t;
+	pthread_mutex_unlock(&g_tune_lock);
 	return 0;
 }
 
@@ -105,7 +113,7 @@ int nkfs_use_device(int dev)
 static int dev_setup_locked(int dev)
 {
 	struct nkfs_dev *d = &g_dev[dev];
-	if (d->ready)
+	if (__atomic_load_n(&d->ready, __ATOMIC_ACQUIRE))
 		return nkfs_use_device(dev);
 	hipError_t e = hipSetDevice(dev);
 	if (e == hipSuccess)
@@ -120,7 +128,9 @@ static int dev_setup_locked(int dev)
 		d->gf = NULL;
 		return rc;
 	}
-	d->ready = 1;
+	/* publish: gf is written before ready reads 1 (nkfs_gf_on reads ready
+	 * outside the lock) */
+	__atomic_store_n(&d->ready, 1, __ATOMIC_RELEASE);
 	return 0;
 }
 
@@ -161,15 +171,17 @@ int nkfs_gpu_init(int device)
 	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
 		g_cus = cus;
 	g_device = device;
-	g_ready = 1;
+	__atomic_store_n(&g_ready, 1, __ATOMIC_RELEASE); /* after g_device, g_cus */
 out:
 	pthread_mutex_unlock(&g_lock);
 	return rc;
 }
 
-int nkfs_gpu_ready(void) { return g_ready; }
+static int ready_now(void) { return __atomic_load_n(&g_ready, __ATOMIC_ACQUIRE); }
 
-int nkfs_gpu_device(void) { return g_ready ? g_device : -1; }
+int nkfs_gpu_ready(void) { return ready_now(); }
+
+int nkfs_gpu_device(void) { return ready_now() ? g_device : -1; }
 
 int nkfs_gpu_count(void) { return device_count(); }
 
@@ -180,7 +192,7 @@ const void *nkfs_gf_on(int dev)
 {
 	if (dev < 0 || dev >= NKFS_MAX_DEVICES)
 		return NULL;
-	if (g_dev[dev].ready)
+	if (__atomic_load_n(&g_dev[dev].ready, __ATOMIC_ACQUIRE))
 		return g_dev[dev].gf;
 	pthread_mutex_lock(&g_lock);
 	int cur = -1;
@@ -206,13 +218,13 @@ const void *nkfs_gf_for(void *stream)
 	return nkfs_gf_on(dev);
 }
 
-const void *nkfs_gf(void) { return g_ready ? g_dev[g_device].gf : NULL; }
+const void *nkfs_gf(void) { return ready_now() ? g_dev[g_device].gf : NULL; }
 
 int nkfs_gpu_set_devices(const int *devices, int count)
 {
 	if (count < 0 || count > NKFS_MAX_DEVICES || (count && !devices))
 		return -EINVAL;
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	const int ndev = device_count();
 	for (int i = 0; i < count; i++)
@@ -238,7 +250,7 @@ int nkfs_gpu_set_devices(const int *devices, int count)
 int nkfs_gpu_get_devices(int *devices, int max)
 {
 	pthread_mutex_lock(&g_lock);
-	int n = g_nlanes ? g_nlanes : (g_ready ? 1 : 0);
+	int n = g_nlanes ? g_nlanes : (ready_now() ? 1 : 0);
 	for (int i = 0; i < n && i < max && devices; i++)
 		devices[i] = g_nlanes ? g_lanes[i] : g_device;
 	pthread_mutex_unlock(&g_lock);
@@ -248,6 +260,8 @@ int nkfs_gpu_get_devices(int *devices, int max)
 static void ctx_destroy(struct nkfs_ctx *c)
 {
 	hipStreamSynchronize(c->stream);
+	for (int i = 0; i < c->nev; i++)
+		hipEventDestroy(c->ev[i]);
 	hipStreamDestroy(c->stream);
 	hipFree(c->dbuf);
 	hipHostFree(c->hbuf);
@@ -283,9 +297,9 @@ void nkfs_gpu_release(void)
 			hipSetDevice(d);
 			hipFree(g_dev[d].gf);
 			g_dev[d].gf = NULL;
-			g_dev[d].ready = 0;
+			__atomic_store_n(&g_dev[d].ready, 0, __ATOMIC_RELEASE);
 		}
-	g_ready = 0;
+	__atomic_store_n(&g_ready, 0, __ATOMIC_RELEASE);
 	g_nlanes = 0;
 	pthread_mutex_unlock(&g_lock);
 }
@@ -300,7 +314,7 @@ void nkfs_ctx_trim(void)
 	}
 	pthread_mutex_unlock(&g_lock);
 	pools_drain(taken);
-	if (g_ready)
+	if (ready_now())
 		nkfs_use_device(g_device);
 }
 
@@ -309,7 +323,7 @@ void nkfs_ctx_trim(void)
 struct nkfs_ctx *nkfs_ctx_get_on(int dev)
 {
 	struct nkfs_ctx *c = NULL;
-	if (!g_ready || dev < 0 || dev >= NKFS_MAX_DEVICES || !nkfs_gf_on(dev))
+	if (!ready_now() || dev < 0 || dev >= NKFS_MAX_DEVICES || !nkfs_gf_on(dev))
 		return NULL;
 	pthread_mutex_lock(&g_lock);
 	if (g_dev[dev].pool) {
@@ -336,7 +350,7 @@ fail:
 
 struct nkfs_ctx *nkfs_ctx_get(void)
 {
-	return g_ready ? nkfs_ctx_get_on(g_device) : NULL;
+	return ready_now() ? nkfs_ctx_get_on(g_device) : NULL;
 }
 
 void nkfs_ctx_put(struct nkfs_ctx *c)
@@ -365,6 +379,15 @@ int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out)
 		c->dcap = cap;
 	}
 	*out = c->dbuf;
+	return 0;
+}
+
+int nkfs_ctx_events(struct nkfs_ctx *c)
+{
+	while (c->nev < 2) {
+		HIPCHK(hipEventCreateWithFlags(&c->ev[c->nev], hipEventDisableTiming));
+		c->nev++;
+	}
 	return 0;
 }
 
@@ -409,7 +432,7 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 {
 	if (nkfs_bad_params(block_size, n, k))
 		return -EINVAL;
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!nstripes)
 		return 0;
@@ -430,7 +453,7 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 {
 	if (nkfs_bad_params(max_block_size, n, k))
 		return -EINVAL;
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!nstripes)
 		return 0;
@@ -456,7 +479,7 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 {
 	if (nkfs_bad_params(block_size, navail, k) || n_slots < 1 || n_slots > 255)
 		return -EINVAL;
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!nstripes)
 		return 0;
@@ -488,7 +511,7 @@ static int decode_ragged_common(const uint8_t *d_parts, const uint64_t *d_part_o
 {
 	if (nkfs_bad_params(max_block_size, navail, k) || n_slots < 1 || n_slots > 255)
 		return -EINVAL;
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!nstripes)
 		return 0;
@@ -539,7 +562,7 @@ int nkfs_nk8_decode_verify(const uint8_t *d_parts, uint64_t part_pitch, int n_sl
 int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off, const uint64_t *d_len, uint32_t count,
 		     uint64_t seed, uint64_t *d_out, void *stream)
 {
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (count && (!d_base || !d_off || !d_len || !d_out))
 		return -EINVAL;
@@ -549,7 +572,7 @@ int nkfs_xxh64_batch(const uint8_t *d_base, const uint64_t *d_off, const uint64_
 int nkfs_clu_sum_batch(const uint8_t *d_clusters, uint64_t cluster_pitch, uint32_t cluster_size, uint32_t count,
 		       uint64_t *d_sums, const uint64_t *d_expect, int32_t *d_status, void *stream)
 {
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!count)
 		return 0;
@@ -565,7 +588,7 @@ int nkfs_pages_dsum_batch(const uint8_t *const *d_pages, const uint64_t *d_first
 {
 	uint32_t shift = 0;
 
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (!count)
 		return 0;
@@ -582,7 +605,7 @@ int nkfs_pages_dsum_batch(const uint8_t *const *d_pages, const uint64_t *d_first
 int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_size, uint32_t nstripes,
 		      uint64_t seed, uint64_t first_stripe, void *stream)
 {
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (nstripes && (!d_blocks || (nstripes > 1 && block_pitch < block_size)))
 		return -EINVAL;
@@ -592,7 +615,7 @@ int nkfs_synth_blocks(uint8_t *d_blocks, uint64_t block_pitch, uint32_t block_si
 int nkfs_synth_ragged(uint8_t *d_blocks, const uint64_t *d_block_off, const uint32_t *d_block_size,
 		      uint32_t nstripes, uint64_t seed, uint64_t first_stripe, void *stream)
 {
-	if (!g_ready)
+	if (!ready_now())
 		return -EAGAIN;
 	if (nstripes && (!d_blocks || !d_block_off || !d_block_size))
 		return -EINVAL;
@@ -602,7 +625,7 @@ int nkfs_synth_ragged(uint8_t *d_blocks, const uint64_t *d_block_off, const uint
 void *nkfs_dev_alloc(size_t bytes)
 {
 	void *p = NULL;
-	if (!g_ready || nkfs_use_device(g_device) || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess)
+	if (!ready_now() || nkfs_use_device(g_device) || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess)
 		return NULL;
 	return p;
 }

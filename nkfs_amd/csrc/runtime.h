@@ -16,6 +16,9 @@ struct nkfs_ctx {
 	size_t dcap;
 	void *hbuf;   /* pinned host scratch */
 	size_t hcap;
+	hipEvent_t ev[2]; /* created on first use (nkfs_ctx_events) */
+	int nev;
+	uint64_t seq;     /* completion words handed out on this context */
 	struct nkfs_ctx *next;
 };
 
@@ -24,6 +27,7 @@ struct nkfs_ctx *nkfs_ctx_get_on(int dev);
 void nkfs_ctx_put(struct nkfs_ctx *c);
 int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out);
+int nkfs_ctx_events(struct nkfs_ctx *c); /* c->ev[0..1] exist afterwards */
 const void *nkfs_gf(void);                   /* tables on the library's device */
 const void *nkfs_gf_on(int dev);
 const void *nkfs_gf_for(void *stream);       /* tables on the device of `stream` */

@@ -83,3 +83,22 @@ def test_part_geometry():
     assert L.nkfs_part_pitch(1048576, 5) == 209920
     assert L.nkfs_part_size(4096, 2) == 2048
     assert L.nkfs_part_pitch(1, 2) == 256
+
+
+def test_walk_offset_bound():
+    """The walk encoder drops a store by setting bit 31 of its buffer offset,
+    so every offset it forms must stay below 2^31 (the digest
+    array's bound was 2^32).  Host-side check, no GPU needed."""
+    import ctypes as C
+    from nkfs_amd import _lib
+    f = _lib.lib().nkfs_walk_offsets_fit
+    f.restype = C.c_int
+    f.argtypes = [C.c_uint64] * 4
+    assert f(1 << 20, 8 * 209920, 8192, 8) == 1
+    # digests: nstripes * n * 8 bytes
+    assert f(4096, 4 * 2048, (1 << 31) // 64 - 1, 8) == 1
+    assert f(4096, 4 * 2048, (1 << 31) // 64, 8) == 0
+    assert f(4096, 4 * 2048, (1 << 28) + 1, 1) == 0
+    # a stripe's part span and the block reach
+    assert f(4096, (1 << 31), 1, 8) == 0
+    assert f((1 << 31) - 2048 * 8, 16, 1, 2) == 0

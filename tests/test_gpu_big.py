@@ -1,0 +1,184 @@
+"""GPU parity of the column-chunked kernels for k > 16 (nk8_big.hip,
+NKFS_ENC_BIG / NKFS_DEC_BIG): the default for k > 16, any n <= 255 and
+k <= 254 (crt/nk8.c:13-16; the reference's self test draws k up to 254,
+crt/nk8.c:735-744).
+
+Every case is checked bit-exact against the thread-per-row general kernels
+(NKFS_ENC_GENERIC / NKFS_DEC_GENERIC) on all stripes and against the oracle
+(oracle/nk8_port.c, pinned to the compiled reference) on sampled stripes:
+one and several 16-column chunks, part groups of 16 (the last one partial),
+k = n, k = 254 / n = 255, tails of every size, unaligned ragged offsets,
+one-byte blocks, the small-k shapes pinned to the big kernels, the
+first-k-distinct selection and the -EINVAL stripe.
+"""
+import numpy as np
+import pytest
+
+from nkfs_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nkfs_amd import _lib
+    lib = _lib.lib()
+    assert lib.nk8_init() == 0, "nk8_init (GPU self test) failed"
+    return lib
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def u64(x):
+    return int(x) & 0xFFFFFFFFFFFFFFFF
+
+
+def _tuned(**kw):
+    from nkfs_amd import _lib
+    return _lib.tuned(**kw)
+
+
+@pytest.mark.parametrize("n,k,B,S", [
+    (48, 32, 1048576, 3),      # the bench's W2 shape: 2 chunks, 3 groups, slices
+    (20, 17, 65536, 10),       # 2 chunks, the second one column wide
+    (255, 254, 70001, 2),      # 16 chunks, 16 groups (the last 15 parts wide)
+    (40, 33, 4099, 30),        # tail rows, k not a multiple of 4
+    (18, 17, 1, 5),            # one-byte blocks
+    (64, 50, 1000003, 2),      # B not a multiple of 4 / 16 / k
+    (17, 17, 17 * 300 + 5, 7),  # k = n
+    (16, 12, 65536, 10),       # k <= 16 pinned to the big kernel
+    (8, 5, 4096, 50),          # n <= 8 pinned to the big kernel
+])
+def test_big_encode_matches(L, O, n, k, B, S):
+    from nkfs_amd import _lib, batch
+    blocks = batch.synth(S, B, first=300 + n)
+    ids_np = synth.batch_ids(S, n, first=300 + n)
+    ids = dev(ids_np)
+    with _tuned(enc_kernel=_lib.ENC["generic"]):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_lib.ENC["big"]):
+        p1, d1 = batch.encode(blocks, B, n, k, ids)
+    p2, d2 = batch.encode(blocks, B, n, k, ids)  # default dispatch
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    assert torch.equal(p0[:, :ps], p2[:, :ps]) and torch.equal(d0, d2)
+    got = [u64(x) for x in d1.cpu().tolist()]
+    for s in sorted({0, S - 1}):
+        want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
+        assert np.array_equal(p1[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), s
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
+
+
+@pytest.mark.parametrize("n,k,gap", [(24, 20, 0), (40, 33, 5), (19, 18, 3)])
+def test_big_encode_ragged(L, O, n, k, gap):
+    """Ragged batches (mixed sizes, block offsets unaligned when gap != 0):
+    the big kernel equals the general kernel, and the oracle per stripe."""
+    from nkfs_amd import _lib, batch
+    sizes = synth.mixed_sizes(16)
+    sizes[:5] = (4096, 65536, 1048576, 1, k + 1)
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos, ppos = 0, 0
+    for s, B in enumerate(sizes):
+        boff[s], poff[s] = pos, ppos
+        pos += int(B) + gap
+        ppos += n * batch.part_pitch(int(B), k)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(500 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=500)
+    outs = []
+    for kern in ("generic", "big"):
+        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+        with _tuned(enc_kernel=_lib.ENC[kern]):
+            batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts,
+                                dev(poff), dig, int(sizes.max()))
+        torch.cuda.synchronize()
+        outs.append((parts.cpu().numpy(), [u64(x) for x in dig.cpu().tolist()]))
+    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    pn, got = outs[1]
+    for s in (0, 2, 3, 4, len(sizes) - 1):
+        B = int(sizes[s])
+        want = O.encode(host[boff[s]: boff[s] + B], n, k, ids_np[s])
+        pitch = batch.part_pitch(B, k)
+        for i in range(n):
+            off = int(poff[s]) + i * pitch
+            assert np.array_equal(pn[off: off + len(want[i])], want[i]), (s, i)
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
+
+
+@pytest.mark.parametrize("n,k,B,S", [
+    (48, 32, 1048576, 3),      # W2 shape
+    (255, 254, 70001, 2),
+    (40, 33, 4099, 30),        # rows of 33 bytes: byte-wise band stores
+    (20, 17, 1000003, 3),
+    (18, 18, 1, 5),            # one-byte blocks, k = n
+    (36, 20, 17 * 1024, 9),
+    (16, 12, 65536, 10),       # k <= 16 pinned to the big decoder
+    (8, 5, 262144, 6),         # k <= 8 pinned to the big decoder
+])
+def test_big_decode_matches(L, O, n, k, B, S):
+    """NKFS_DEC_BIG rebuilds every block like the general decoder from k
+    seeded survivors offered in random order plus one extra slot; stripe 1
+    offers a duplicate id (skipped, crt/nk8.c:512-537), stripe 2 one distinct
+    id (status -EINVAL, block untouched)."""
+    from nkfs_amd import _lib, batch
+    blocks = batch.synth(S, B, first=60 + k)
+    ids_np = synth.batch_ids(S, n, first=60 + k)
+    parts, _ = batch.encode(blocks, B, n, k, dev(ids_np))
+    keep = min(n, k + 1)
+    av = synth.batch_survivors(S, n, keep, first=60 + k)
+    ids2 = ids_np.copy()
+    if S > 2 and keep > k:
+        ids2[1, av[1, 1]] = ids2[1, av[1, 0]]
+    if S > 2:
+        ids2[2, :] = ids2[2, 0]
+    outs = []
+    for kern in ("generic", "big", "auto"):
+        with _tuned(dec_kernel=_lib.DEC[kern]):
+            out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
+            _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
+            torch.cuda.synchronize()
+            outs.append((out.cpu(), st.cpu().tolist()))
+    for o, st in outs[1:]:
+        assert st == outs[0][1]
+        assert torch.equal(o, outs[0][0])
+    o, st = outs[1]
+    ref = blocks[:, :B].cpu()
+    for s in range(S):
+        if S > 2 and s == 2:
+            assert st[s] == -22 and bool((o[s] == 0xEE).all())
+        else:
+            assert st[s] == 0 and torch.equal(o[s], ref[s]), s
+    s = S - 1
+    sel = [int(x) for x in av[s]]
+    pn = parts[s * n:(s + 1) * n, :batch.part_size(B, k)].cpu().numpy()
+    got = O.decode([pn[j] for j in sel], [int(ids_np[s, j]) for j in sel], k, B)
+    assert np.array_equal(np.asarray(got), ref[s].numpy())
+
+
+def test_big_round_trip_w2(L):
+    """The bench's W2 batch (256 x 1 MiB, N48K32): default encode -> keep 32
+    seeded survivors -> default decode gives every block back."""
+    from nkfs_amd import batch
+    S, B, n, k = 256, 1048576, 48, 32
+    blocks = batch.synth(S, B, first=11)
+    ids = dev(synth.batch_ids(S, n, first=11))
+    parts, _ = batch.encode(blocks, B, n, k, ids)
+    avail = dev(synth.batch_survivors(S, n, k, first=11))
+    out, status = batch.decode(parts, n, ids, avail, k, B)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])

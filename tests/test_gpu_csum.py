@@ -1,0 +1,153 @@
+"""GPU parity of the per-call checksum ABI (crt/csum.c:3-27,
+crt/xxhash.c:566-930; csum.c + xxh64_chain.hip): one GPU round trip per
+message, messages pending on the GPU between XXH64_update and
+XXH64_digest.
+
+Checked against the oracle's XXH64 (oracle/nk8_port.c, pinned to the
+compiled reference and the python xxhash package): long streams (20 MiB,
+and 8 MiB + 17 bytes after a 5-byte partial update) across the
+256 KiB fold chunks, random chunkings, more pending states than slots (the
+synchronous fallback), digest-then-continue (the reference's digest leaves
+the state usable), reset / free of a pending state, seeds, and threads.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nkfs_amd import _lib
+    lib = _lib.lib()
+    assert lib.nk8_init() == 0
+    return lib
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+
+def _state(L, seed=0):
+    st = L.XXH64_createState()
+    assert st
+    assert L.XXH64_reset(st, seed) == 0
+    return st
+
+
+def _upd(L, st, a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    assert L.XXH64_update(st, a.ctypes.data if a.size else None, a.size) == 0
+
+
+def test_long_streams(L, O):
+    from nkfs_amd import crt
+    rng = np.random.default_rng(21)
+    data = rng.integers(0, 256, (20 << 20) + 7, dtype=np.uint8)
+    want = O.xxh64(data)
+    assert crt.xxh64(data) == want                      # one-shot
+    st = _state(L)
+    _upd(L, st, data)                                    # one update
+    assert L.XXH64_digest(st) == want
+    L.XXH64_freeState(st)
+    # 5-byte partial, then 8 MiB + 17 in one update, then the rest
+    cs = crt.Csum()
+    cs.update(data[:5])
+    cs.update(data[5: 5 + (8 << 20) + 17])
+    cs.update(data[5 + (8 << 20) + 17:])
+    assert cs.digest() == want
+    # random chunk sizes across the 256 KiB fold boundaries
+    cs = crt.Csum()
+    pos = 0
+    while pos < data.size:
+        step = int(rng.choice([1, 31, 33, 4096, 262143, 262144, 262177, 1 << 20]))
+        cs.update(data[pos: pos + step])
+        pos += step
+    assert cs.digest() == want
+
+
+@pytest.mark.parametrize("seed", [0, 1, 0x9E3779B185EBCA87, (1 << 64) - 1])
+def test_seeds_and_lengths(L, O, seed):
+    rng = np.random.default_rng(seed & 0xFFFF)
+    for n in [0, 1, 31, 32, 33, 63, 64, 65, 262144 - 1, 262144, 262144 + 31, 262144 + 33, 3 * 262144 + 5]:
+        data = rng.integers(0, 256, n, dtype=np.uint8)
+        st = _state(L, seed)
+        _upd(L, st, data)
+        assert L.XXH64_digest(st) == O.xxh64(data, seed), n
+        L.XXH64_freeState(st)
+
+
+def test_digest_then_continue(L, O):
+    """The reference's digest does not end the state (crt/xxhash.c:838-930):
+    updates after a digest continue the same message."""
+    rng = np.random.default_rng(4)
+    a = rng.integers(0, 256, 100000, dtype=np.uint8)
+    b = rng.integers(0, 256, 300001, dtype=np.uint8)
+    st = _state(L)
+    _upd(L, st, a)
+    assert L.XXH64_digest(st) == O.xxh64(a)
+    assert L.XXH64_digest(st) == O.xxh64(a)  # twice
+    _upd(L, st, b)
+    assert L.XXH64_digest(st) == O.xxh64(np.concatenate([a, b]))
+    L.XXH64_freeState(st)
+
+
+def test_reset_and_free_pending(L, O):
+    rng = np.random.default_rng(6)
+    a = rng.integers(0, 256, 70000, dtype=np.uint8)
+    st = _state(L)
+    _upd(L, st, a)                 # pending on the GPU
+    assert L.XXH64_reset(st, 7) == 0  # abandons it
+    _upd(L, st, a[:1000])
+    assert L.XXH64_digest(st) == O.xxh64(a[:1000], 7)
+    st2 = _state(L)
+    _upd(L, st2, a)
+    L.XXH64_freeState(st2)         # freed while pending: the slot is released
+
+
+def test_more_pending_states_than_slots(L, O):
+    """1,100 messages pending at once (1,024 slots): the rest fold
+    synchronously; every digest, taken in reverse order, is exact."""
+    from nkfs_amd import crt
+    rng = np.random.default_rng(8)
+    datas = [rng.integers(0, 256, int(rng.integers(32, 3000)), dtype=np.uint8) for _ in range(1100)]
+    cs = []
+    for d in datas:
+        c = crt.Csum()
+        c.update(d[:40])
+        c.update(d[40:])
+        cs.append(c)
+    for c, d in reversed(list(zip(cs, datas))):
+        assert c.digest() == O.xxh64(d)
+
+
+def test_threads(L, O):
+    """Eight host threads hash concurrently (ctypes drops the GIL): per-call
+    contexts and slots are per message, the results exact."""
+    from nkfs_amd import crt
+    rng = np.random.default_rng(9)
+    datas = [rng.integers(0, 256, int(rng.integers(1, 600000)), dtype=np.uint8) for _ in range(64)]
+    want = [O.xxh64(d) for d in datas]
+    got = [None] * len(datas)
+
+    def work(t):
+        for i in range(t, len(datas), 8):
+            if i % 2:
+                got[i] = crt.xxh64(datas[i])
+            else:
+                c = crt.Csum()
+                for j in range(0, datas[i].size, 77777):
+                    c.update(datas[i][j: j + 77777])
+                got[i] = c.digest()
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == want
