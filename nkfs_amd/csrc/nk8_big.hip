@@ -27,9 +27,9 @@
 //                slice) are dispatched back to back on one XCD (workgroup b
 //                runs on XCD b mod 8) and share the block's lines in its L2.
 //  k_decode_big  workgroup = (stripe, group of 16 output columns, slice of
-//                1,024 rows); a chunk's survivor bytes by byte loads (64
-//                consecutive bytes of one part per wave instruction) into an
-//                LDS row stage; a lane writes its row's 16 columns, and the
+//                1,024 rows); a chunk's 16 survivor parts over the slice by
+//                16-byte loads (1 KiB contiguous per part) into an LDS
+//                [survivor][row] stage; a lane writes its row's 16 columns, and the
 //                groups of a (stripe, slice) run back to back on one XCD so
 //                the rows' lines complete in its L2.
 // XXH64 of the parts is the batched message hash afterwards (a part's chain
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
                                                        u32 ngroups, u32 nslices)
 {
     __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];
-    __shared__ __attribute__((aligned(16))) uint4 ins[DEC_T][256];  // a chunk's survivor bytes per row
+    __shared__ __attribute__((aligned(16))) u8 ins[16 * DEC_ROWS];  // a chunk's survivor bytes, [survivor][row]
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
     const u32 h = loc % ngroups;
@@ -236,6 +236,7 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
     const int k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const u8 *wk = work + u64(s) * u64(k + k * k);
+    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
 
     uint4 acc[DEC_T];
 #pragma unroll
@@ -245,21 +246,31 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
     const int nch = (k + 15) / 16;
     for (int cc = 0; cc < nch; ++cc) {
         __syncthreads();  // the previous chunk's tables and rows are consumed
-        // survivor bytes of columns 16cc.. of my rows (one row per lane per
-        // t; a wave instruction reads 64 consecutive bytes of one part),
-        // packed into the LDS row stage
-#pragma unroll 1
-        for (int t = 0; t < DEC_T; ++t) {
-            const u32 r = r_begin + u32(t) * 256u + u32(tid);
-            u32 w[4] = {0, 0, 0, 0};
-            if (r < v.ps)
+        // the chunk's 16 survivor parts over the slice's rows, staged in LDS
+        // as [survivor][row]: thread t moves 64 rows of survivor t / 16
+        // (four 16-byte loads; 16 threads = 1 KiB contiguous of one part)
+        {
+            const int j = tid >> 4, c = 16 * cc + j;
+            const u32 r0 = r_begin + 64u * u32(tid & 15);
+            const bool live = c < k;
+            const u8 *src = live ? v.parts + u64(wk[c]) * v.pitch : v.parts;
+            uint4 x[DEC_T];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int c = 16 * cc + j;
-                    if (c < k)
-                        w[j >> 2] |= u32(v.parts[u64(wk[c]) * v.pitch + r]) << (8 * (j & 3));
+            for (int q = 0; q < DEC_T; ++q) {
+                const u32 r = r0 + 16u * q;
+                if (live && pal && r + 16 <= v.ps) {
+                    x[q] = *reinterpret_cast<const uint4 *>(src + r);
+                } else {
+                    u32 w[4] = {0, 0, 0, 0};
+                    if (live)
+                        for (u32 e = 0; e < 16 && r + e < v.ps; ++e)
+                            w[e >> 2] |= u32(src[r + e]) << (8 * (e & 3));
+                    x[q] = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-            ins[t][tid] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < DEC_T; ++q)
+                *reinterpret_cast<uint4 *>(ins + j * DEC_ROWS + 64u * u32(tid & 15) + 16u * q) = x[q];
         }
         // table j: survivor 16cc+j, U_j[x] = (W[c][16h] x, ..., W[c][16h+15] x)
 #pragma unroll 1
@@ -280,12 +291,11 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
         u32 tdep = 0;  // 0 at run time: one row's lookups in flight at a time
 #pragma unroll
         for (int t = 0; t < DEC_T; ++t) {
-            const uint4 iv = ins[t][tid];
-            const u32 in[4] = {iv.x, iv.y, iv.z, iv.w};
+            const u32 rl = u32(t) * 256u + u32(tid);  // row within the slice
             uint4 e = acc[t];
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const u32 byte = (in[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                const u32 byte = ins[j * DEC_ROWS + rl];
                 const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
                 e.x ^= tv.x;
                 e.y ^= tv.y;

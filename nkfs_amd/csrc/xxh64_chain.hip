@@ -4,12 +4,12 @@
 //
 // One message has exactly four dependent chains of rounds (the accumulators,
 // crt/xxhash.c:791-810), so one wave folds it: lane a runs accumulator a
-// (lanes 4.. mirror lane a & 3 and are ignored).  Each lane keeps the words
-// of the next D stripes in flight in a register ring -- loads are issued D
-// rounds ahead, straight from the caller-staged pinned host buffer over
-// PCIe (no copy engine, no host-side wait) or from device memory -- so a
-// round waits only on the previous round (~96 SIMD cycles, tools/sol.hip).
-// No LDS, no barrier.  The same launch can start from accumulators passed
+// (lanes 4.. mirror lane a & 3 and are ignored), reading the message
+// straight from the caller-staged pinned host buffer over PCIe (no copy
+// engine, no host-side wait) or from device memory, far enough ahead that
+// a round waits only on the previous round (~80-100 SIMD cycles,
+// tools/sol.hip): 32 bytes per round per chain, so a 64 KiB message is
+// 2,048 dependent rounds and 1 MiB 32,768.  No barrier.  The same launch can start from accumulators passed
 // by value or kept on the device, leave them on the device (a long stream
 // folded chunk by chunk), and finish: merge, length, the <32-byte tail
 // passed by value, avalanche, then the digest and a completion word stored
@@ -29,32 +29,84 @@ namespace {
 typedef uint64_t u64;
 typedef uint32_t u32;
 typedef uint8_t u8;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
-constexpr int D = 48;  // rounds of loads in flight per lane (vmcnt holds 63)
+// The message streams through an LDS ring of NS slots of 1 KiB (32
+// stripes): each slot is one global_load_lds_dwordx4 of the whole wave (no
+// VGPR staging), issued NS-1 slots ahead -- 31 KiB in flight, so the PCIe
+// latency of pinned host memory (several us) hides under ~500 rounds -- and
+// waited for with a counted vmcnt (the loop issues no other vector memory
+// instruction).  Lane a then reads its 32 words of the slot (ds_read_b64)
+// and runs its 32 rounds.
+constexpr int NS = 32;
 
 __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
 {
-    const int lane = threadIdx.x & 3;
-    u64 acc = (a.flags & NKFS_XXH_FROM_DEV) ? a.v_dev[lane] : a.v[lane];
+    __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
+    const int li = threadIdx.x, lane = li & 3;
+    // (selects, not a.v[lane]: a dynamically indexed kernel argument goes
+    // through scratch)
+    u64 acc = lane == 0 ? a.v[0] : lane == 1 ? a.v[1] : lane == 2 ? a.v[2] : a.v[3];
+    if (a.flags & NKFS_XXH_FROM_DEV)
+        acc = a.v_dev[lane];
     const u64 nst = a.nst;
-    const u8 *src = a.src + 8 * lane;
-    // word of stripe i; stripes past the end read stripe 0 (unused): every
-    // slot is loaded unconditionally, so the in-order vmcnt waits are exact
-    auto ld = [&](u64 i) { return *reinterpret_cast<const u64 *>(src + 32 * (i < nst ? i : 0)); };
+    const u64 nslots = (nst + 31) / 32;
+    // slot c = stripes 32c..32c+31; lane li moves bytes 16li..16li+15 of it
+    // (slots past the message read its first KiB again: unused)
+    auto issue = [&](u64 c) {
+        const u64 off = c < nslots ? c * 1024 + 16 * li : 16 * li;
+        const u8 *src = a.src + (off + 16 <= nst * 32 ? off : 0);
+        __builtin_amdgcn_global_load_lds((const void *)src,
+                                         (__attribute__((address_space(3))) void *)(ring + (c % NS) * 1024), 16,
+                                         0, 0);
+    };
     if (nst) {
-        u64 ring[D];
 #pragma unroll
-        for (int j = 0; j < D; ++j)
-            ring[j] = ld(u64(j));
-        for (u64 base = 0; base < nst; base += D) {
+        for (int c = 0; c < NS - 1; ++c)
+            issue(u64(c));
+        // full slots: no per-round select on the chain's critical path
+        const u64 nfull = nst / 32;
+        for (u64 c = 0; c < nslots; ++c) {
+            issue(c + NS - 1);  // into the slot slot c-1 was read from
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+            // The multiplies by P2 do not depend on the chain: all 64 lanes
+            // take them for the whole slot (two words each, in place), so
+            // the four chain lanes' rounds are add, rotate, multiply by P1.
+            // A wave issues its 64-bit multiplies for all 64 lanes whatever
+            // the exec mask: this cuts the chain's multiply issue by half.
+            u8 *sb = ring + (c % NS) * 1024;
+            {
+                // read and written back by asm: compiler-visible LDS accesses
+                // here make it wait for every DMA still landing in the ring
+                // (vmcnt(0)); the wave's own LDS operations stay in order, so
+                // the chain lanes' reads below see the products
+                const u32 la = u32(reinterpret_cast<uintptr_t>(
+                    (__attribute__((address_space(3))) u8 *)(sb + 16 * li)));
+                v4u q;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(q) : "v"(la) : "memory");
+                const u64 m0 = ((u64(q.y) << 32) | q.x) * XP2, m1 = ((u64(q.w) << 32) | q.z) * XP2;
+                const v4u mv = {u32(m0), u32(m0 >> 32), u32(m1), u32(m1 >> 32)};
+                asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(mv) : "memory");
+            }
+            const u8 *slot = sb + 8 * lane;
+            u64 w[32];
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const u64 w = ring[j];
-                ring[j] = ld(base + D + j);
-                const u64 nx = xxh_round(acc, w);
-                acc = base + j < nst ? nx : acc;
+            for (int r = 0; r < 32; ++r)
+                w[r] = *reinterpret_cast<const u64 *>(slot + 32 * r);
+            if (c < nfull) {
+#pragma unroll
+                for (int r = 0; r < 32; ++r)
+                    acc = rotl64_31(acc + w[r]) * XP1;
+            } else {
+                const u32 left = u32(nst - c * 32);
+#pragma unroll
+                for (int r = 0; r < 32; ++r) {
+                    const u64 nx = rotl64_31(acc + w[r]) * XP1;
+                    acc = u32(r) < left ? nx : acc;
+                }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
     }
     if (a.flags & NKFS_XXH_TO_DEV)
         if (threadIdx.x < 4)

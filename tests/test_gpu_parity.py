@@ -784,3 +784,35 @@ def test_ragged_slice_decode_matches_wave(L, n, k, units):
     for s, B in enumerate(sizes):
         if s != 3:
             assert st[s] == 0 and np.array_equal(o[boff[s]: boff[s] + B].numpy(), host[boff[s]: boff[s] + B]), s
+
+
+@pytest.mark.parametrize("S,B", [(512, 1048576), (1024, 1048576), (512, 262144)])
+def test_bench_kernels_against_oracle(L, O, S, B):
+    """The kernels the bench times, pinned through struct nkfs_tune and
+    compared with the oracle directly (not only with another kernel): the
+    warp-specialised encoder (C3's default) and the walk encoder (C4's) on
+    >= 512 stripes -- every part's bytes and XXH64 of a 16-stripe sample
+    spread over the batch -- and the one-shot slice decoder rebuilding every
+    block from the seeded 5-of-8 survivors (crt/nk8.c:344-444, 446-599)."""
+    from nkfs_amd import batch
+    n, k = 8, 5
+    blocks = batch.synth(S, B, first=4242)
+    ids_np = synth.batch_ids(S, n, first=4242)
+    ids = dev(ids_np)
+    ps = batch.part_size(B, k)
+    sample = sorted({int(x) for x in np.linspace(0, S - 1, 16)})
+    for kern in ("ws", "walk"):
+        with _tuned(enc_kernel=_enc(kern)):
+            parts, dig = batch.encode(blocks, B, n, k, ids)
+        torch.cuda.synchronize()
+        got = [u64(x) for x in dig.cpu().tolist()]
+        for s in sample:
+            want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
+            assert np.array_equal(parts[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), (kern, s)
+            assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], (kern, s)
+    avail = dev(synth.batch_survivors(S, n, k, first=4242))
+    with _tuned(dec_kernel=_dec("slice")):
+        out, status = batch.decode(parts, n, ids, avail, k, B)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])
