@@ -27,9 +27,10 @@
 //                slice) are dispatched back to back on one XCD (workgroup b
 //                runs on XCD b mod 8) and share the block's lines in its L2.
 //  k_decode_big  workgroup = (stripe, group of 16 output columns, slice of
-//                1,024 rows); a chunk's 16 survivor parts over the slice by
-//                16-byte loads (1 KiB contiguous per part) into an LDS
-//                [survivor][row] stage; a lane writes its row's 16 columns, and the
+//                4,096 rows); a chunk's 16 survivor parts come through an
+//                LDS [row][survivor] stage 512 rows at a time (coalesced
+//                dword loads, 4x4 byte transposes); a lane writes its
+//                rows' 16 columns, and the
 //                groups of a (stripe, slice) run back to back on one XCD so
 //                the rows' lines complete in its L2.
 // XXH64 of the parts is the batched message hash afterwards (a part's chain
@@ -37,6 +38,8 @@
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "nk8_dev.h"
 
@@ -56,12 +59,12 @@ __device__ inline __amdgpu_buffer_rsrc_t brsrc(const void *base, u32 bytes)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
 }
 
-// x^e over GF(2^8) for x != 0 by the log/antilog tables (x^0 = 1)
-__device__ inline u32 gf_pow(const GfTables *t, u32 x, u32 e)
+// x^e over GF(2^8) by the log/antilog tables staged in LDS (x^0 = 1)
+__device__ inline u32 gf_pow(const uint16_t *lg, const u8 *ex, u32 x, u32 e)
 {
     if (!x)
         return e ? 0u : 1u;
-    return t->exp[(u32(t->log[x]) * e) % 255u];
+    return ex[(u32(lg[x]) * e) % 255u];
 }
 
 __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *ids, const GfTables *gft,
@@ -70,6 +73,8 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];   // 16 tables of 256 x 16 B
     __shared__ __attribute__((aligned(16))) u32 stage[4 * 256];      // [part quad][row]
     __shared__ __attribute__((aligned(16))) uint4 coef[256];         // coef[m] = (x_{p0+e}^m), e < 16
+    __shared__ uint16_t glog[256];
+    __shared__ u8 gexp[256];
 
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
@@ -87,13 +92,23 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     const int p0 = int(grp) * 16, np = min(16, n - p0);
 
     // Vandermonde rows of the group's parts: coef[m] byte e = x_{p0+e}^m
-    // (crt/nk8.c:404-406 builds the same powers by repeated multiplication)
+    // (crt/nk8.c:404-406 builds the same powers by repeated multiplication),
+    // from log/antilog tables staged in LDS
+    glog[tid] = gft->log[tid];
+    gexp[tid] = gft->exp[tid];
+    __syncthreads();
     {
         const u8 *sid = ids + u64(s) * u64(n) + p0;
+        u32 xs[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            xs[e] = e < np ? sid[e] : 0u;
         for (int m = tid; m < k; m += 256) {
             u32 w[4] = {0, 0, 0, 0};
-            for (int e = 0; e < np; ++e)
-                w[e >> 2] |= gf_pow(gft, sid[e], u32(m)) << (8 * (e & 3));
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                if (e < np)
+                    w[e >> 2] |= gf_pow(glog, gexp, xs[e], u32(m)) << (8 * (e & 3));
             coef[m] = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
@@ -126,54 +141,67 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
         // tdep (0 at run time) chains each row's lookups and the next row's
         // loads behind the previous row's XORs: unchained, the compiler
         // hoists all 16 rows' loads and 256 lookups and spills
-        u32 tdep = 0;
-        auto load = [&](int t, v4u &x, u32 &x4, u32 &pos) {
-            const u32 r = r_begin + u32(t) * 256u + u32(tid);
-            pos = r * u32(k) + 16u * u32(cc);  // block byte of column 16cc of row r
-            const u32 a = (pos + mis + tdep) & ~3u;
-            x = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
-            x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
-        };
-        v4u xc, xn;
-        u32 x4c, x4n, posc, posn;
-        load(0, xc, x4c, posc);
+        // only the slice holding the stripe's last row reads bytes past B:
+        // the masking is compiled into a second copy of the row loop
+        const bool tail = (u64(r_begin) + ENC_ROWS) * u64(k) > u64(v.B);
+        auto rows = [&](auto mask) {
+            constexpr bool MASK = decltype(mask)::value;
+            // tdep (0 at run time) chains each row's lookups and the next
+            // row's loads behind the previous row's XORs: unchained, the
+            // compiler hoists all 16 rows' loads and 256 lookups and spills
+            u32 tdep = 0;
+            auto load = [&](int t, v4u &x, u32 &x4, u32 &pos) {
+                const u32 r = r_begin + u32(t) * 256u + u32(tid);
+                pos = r * u32(k) + 16u * u32(cc);  // block byte of column 16cc of row r
+                const u32 a = (pos + mis + tdep) & ~3u;
+                x = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+                x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
+            };
+            v4u xc, xn;
+            u32 x4c, x4n, posc, posn;
+            load(0, xc, x4c, posc);
 #pragma unroll
-        for (int t = 0; t < ENC_T; ++t) {
-            if (t + 1 < ENC_T)
-                load(t + 1, xn, x4n, posn);
-            const u32 sh = (posc + mis) & 3u;
-            u32 d[4];
-            d[0] = __builtin_amdgcn_alignbyte(xc.y, xc.x, sh);
-            d[1] = __builtin_amdgcn_alignbyte(xc.z, xc.y, sh);
-            d[2] = __builtin_amdgcn_alignbyte(xc.w, xc.z, sh);
-            d[3] = __builtin_amdgcn_alignbyte(x4c, xc.w, sh);
-            // bytes at or past B are zero (the reference zero-pads its tail
-            // row, crt/nk8.c:393-398); columns past k meet zero tables
-            {
-                // branch-free: a branch here splits the step's block
-                const u32 valid = v.B > posc ? min(v.B - posc, 16u) : 0u;
+            for (int t = 0; t < ENC_T; ++t) {
+                if (t + 1 < ENC_T)
+                    load(t + 1, xn, x4n, posn);
+                const u32 sh = (posc + mis) & 3u;
+                u32 d[4];
+                d[0] = __builtin_amdgcn_alignbyte(xc.y, xc.x, sh);
+                d[1] = __builtin_amdgcn_alignbyte(xc.z, xc.y, sh);
+                d[2] = __builtin_amdgcn_alignbyte(xc.w, xc.z, sh);
+                d[3] = __builtin_amdgcn_alignbyte(x4c, xc.w, sh);
+                if constexpr (MASK) {
+                    // bytes at or past B are zero (the reference zero-pads
+                    // its tail row, crt/nk8.c:393-398); columns past k meet
+                    // zero tables
+                    const u32 valid = v.B > posc ? min(v.B - posc, 16u) : 0u;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
-                    d[w] &= u32((u64(1) << (8 * keep)) - 1u);
+                    for (int w = 0; w < 4; ++w) {
+                        const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
+                        d[w] &= u32((u64(1) << (8 * keep)) - 1u);
+                    }
                 }
-            }
-            uint4 e = acc[t];
+                uint4 e = acc[t];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const u32 byte = (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
-                e.x ^= tv.x;
-                e.y ^= tv.y;
-                e.z ^= tv.z;
-                e.w ^= tv.w;
+                for (int j = 0; j < 16; ++j) {
+                    const u32 byte = (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
+                    e.x ^= tv.x;
+                    e.y ^= tv.y;
+                    e.z ^= tv.z;
+                    e.w ^= tv.w;
+                }
+                acc[t] = e;
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+                xc = xn;
+                x4c = x4n;
+                posc = posn;
             }
-            acc[t] = e;
-            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
-            xc = xn;
-            x4c = x4n;
-            posc = posn;
-        }
+        };
+        if (tail)
+            rows(std::true_type{});
+        else
+            rows(std::false_type{});
     }
 
     // 256 rows x 16 parts per t-unit: [part quad][row] in LDS (conflict-free
@@ -212,16 +240,41 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     }
 }
 
-// Decode: one workgroup per (stripe, group of 16 output columns, slice of
-// 256*DEC_T rows).
-constexpr int DEC_T = 4;  // 64 KiB tables + 16 KiB row stage: two workgroups per CU
-constexpr u32 DEC_ROWS = 256u * DEC_T;
+// Up to 4 bytes (left >= 1; fewer when left < 4) from an unaligned address,
+// byte by byte: ragged batches with unaligned part offsets only.
+// Branch-free (clamped addresses, then a select): conditional loads would
+// cost the common path its registers in exec-mask juggling.
+__device__ __forceinline__ u32 load4_bytes(const u8 *p, u32 left)
+{
+    u32 w = 0;
+#pragma unroll
+    for (u32 e = 0; e < 4; ++e) {
+        const u32 b = p[e < left ? e : left - 1];
+        w |= (e < left ? b : 0u) << (8 * e);
+    }
+    return w;
+}
 
+// Decode: one workgroup per (stripe, group of 16 output columns, slice of
+// 256*DEC_T rows); the survivors come through the LDS stage SUB rows at a
+// time, so a chunk's tables serve the whole slice.
+constexpr int DEC_T = 16;                 // rows per lane per slice
+constexpr u32 DEC_ROWS = 256u * DEC_T;    // 4,096
+constexpr u32 SUB = 512;                  // rows per survivor stage: 64 KiB tables + 10 KiB, two workgroups per CU
+
+// PAL: every stripe's parts 16-byte aligned (the launcher knows it for
+// uniform batches; ragged ones take the byte-wise form)
+template <bool PAL>
 __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *work, const int32_t *status,
                                                        u32 ngroups, u32 nslices)
 {
     __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];
-    __shared__ __attribute__((aligned(16))) u8 ins[16 * DEC_ROWS];  // a chunk's survivor bytes, [survivor][row]
+    // survivor bytes of a sub-block, [row][survivor] at a 20-byte row pitch
+    // (odd in dwords: the transposing byte writes spread over the banks)
+    __shared__ __attribute__((aligned(16))) u8 ins[20 * SUB];
+    // W[16cc+j][16h..16h+15] for a chunk's table build, in the stage (whose
+    // rows are written only after the tables are built)
+    uint4 *const wq = reinterpret_cast<uint4 *>(ins);
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
     const u32 h = loc % ngroups;
@@ -236,7 +289,6 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
     const int k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const u8 *wk = work + u64(s) * u64(k + k * k);
-    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
 
     uint4 acc[DEC_T];
 #pragma unroll
@@ -245,65 +297,105 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
 
     const int nch = (k + 15) / 16;
     for (int cc = 0; cc < nch; ++cc) {
-        __syncthreads();  // the previous chunk's tables and rows are consumed
-        // the chunk's 16 survivor parts over the slice's rows, staged in LDS
-        // as [survivor][row]: thread t moves 64 rows of survivor t / 16
-        // (four 16-byte loads; 16 threads = 1 KiB contiguous of one part)
+        __syncthreads();  // the previous chunk's tables are consumed
         {
-            const int j = tid >> 4, c = 16 * cc + j;
-            const u32 r0 = r_begin + 64u * u32(tid & 15);
-            const bool live = c < k;
-            const u8 *src = live ? v.parts + u64(wk[c]) * v.pitch : v.parts;
-            uint4 x[DEC_T];
-#pragma unroll
-            for (int q = 0; q < DEC_T; ++q) {
-                const u32 r = r0 + 16u * q;
-                if (live && pal && r + 16 <= v.ps) {
-                    x[q] = *reinterpret_cast<const uint4 *>(src + r);
-                } else {
-                    u32 w[4] = {0, 0, 0, 0};
-                    if (live)
-                        for (u32 e = 0; e < 16 && r + e < v.ps; ++e)
-                            w[e >> 2] |= u32(src[r + e]) << (8 * (e & 3));
-                    x[q] = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < DEC_T; ++q)
-                *reinterpret_cast<uint4 *>(ins + j * DEC_ROWS + 64u * u32(tid & 15) + 16u * q) = x[q];
+            // byte e of row j: thread 16j + e (zero past k; clamped loads,
+            // no branch)
+            const int j = tid >> 4, e = tid & 15, c = 16 * cc + j, m = 16 * int(h) + e;
+            const bool live = c < k && m < k;
+            const u8 wv = wk[k + (live ? c * k + m : 0)];
+            reinterpret_cast<u8 *>(wq)[tid] = live ? wv : u8(0);
         }
+        __syncthreads();
         // table j: survivor 16cc+j, U_j[x] = (W[c][16h] x, ..., W[c][16h+15] x)
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
-            const int j = wave + 4 * q, c = 16 * cc + j;
-            u32 row[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = 16 * int(h) + e;
-                if (c < k && m < k)
-                    row[e >> 2] |= u32(wk[k + c * k + m]) << (8 * (e & 3));
-            }
+            const int j = wave + 4 * q;
+            const uint4 wv = wq[j];
+            const u32 row[4] = {wv.x, wv.y, wv.z, wv.w};
             u32 basis[8][4];
             make_basis<4>(basis, row);
             build_table16(tbl + j * 4096, basis, lane);
         }
-        __syncthreads();
-        u32 tdep = 0;  // 0 at run time: one row's lookups in flight at a time
+        // Survivor stage: thread t takes row group rg = t & 127 (rows
+        // 4rg..4rg+3 of the sub-block) of survivor quads t >> 7 and
+        // (t >> 7) + 2: one dword of each of the quad's four parts (a wave
+        // reads 256 contiguous bytes of one part per instruction), a 4x4
+        // byte transpose, and four dword writes into [row][20-byte pitch]
+        // (at most 2-way bank conflicts; the lanes' reads below, at a
+        // 5-dword stride, none).
+        const int rg = tid & 127, sq0 = tid >> 7;
+        const u8 *qsrc[2][4];
+        bool qlive[2][4];
 #pragma unroll
-        for (int t = 0; t < DEC_T; ++t) {
-            const u32 rl = u32(t) * 256u + u32(tid);  // row within the slice
-            uint4 e = acc[t];
+        for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const u32 byte = ins[j * DEC_ROWS + rl];
-                const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
-                e.x ^= tv.x;
-                e.y ^= tv.y;
-                e.z ^= tv.z;
-                e.w ^= tv.w;
+            for (int jj = 0; jj < 4; ++jj) {
+                const int c = 16 * cc + 4 * (sq0 + 2 * b2) + jj;
+                qlive[b2][jj] = c < k;
+                qsrc[b2][jj] = v.parts + (c < k ? u64(wk[c]) * v.pitch : 0);
             }
-            acc[t] = e;
-            asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+        u32 tdep = 0;  // 0 at run time: chains each row's lookups behind the previous row's
+        // Not unrolled (unrolled, the compiler's schedule spills): the rows
+        // of sub-block `sub` are acc[0..SUB/256-1], and the accumulators
+        // rotate by SUB/256 after each sub-block, back in order after all
+#pragma unroll 1
+        for (int sub = 0; sub < int(DEC_ROWS / SUB); ++sub) {
+            const u32 r4 = r_begin + u32(sub) * SUB + 4u * u32(rg);  // first of the thread's 4 rows
+            u32 dq[2][4];
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    // below ps the dword lies inside the part's pitch; bytes
+                    // past ps feed rows that are never stored
+                    const bool ok = qlive[b2][jj] && r4 < v.ps;
+                    if constexpr (PAL)
+                        dq[b2][jj] = ok ? *reinterpret_cast<const u32 *>(qsrc[b2][jj] + r4) : 0u;
+                    else
+                        dq[b2][jj] = ok ? load4_bytes(qsrc[b2][jj] + r4, v.ps - r4) : 0u;
+                }
+            __syncthreads();  // tables built / the previous sub-block's rows consumed
+            u32 *iw = reinterpret_cast<u32 *>(ins);
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2) {
+                u32 o[4];
+                transpose4(dq[b2][0], dq[b2][1], dq[b2][2], dq[b2][3], o[0], o[1], o[2], o[3]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    iw[(4 * rg + i) * 5 + sq0 + 2 * b2] = o[i];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < int(SUB / 256); ++i) {
+                const int t = i;
+                const u32 rl = u32(i) * 256u + u32(tid);  // row within the sub-block
+                const u32 *ip = reinterpret_cast<const u32 *>(ins) + rl * 5;
+                const u32 in[4] = {ip[0], ip[1], ip[2], ip[3]};
+                uint4 e = acc[t];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const u32 byte = (in[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + tdep + j * 4096 + byte * 16);
+                    e.x ^= tv.x;
+                    e.y ^= tv.y;
+                    e.z ^= tv.z;
+                    e.w ^= tv.w;
+                }
+                acc[t] = e;
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+            }
+            constexpr int R = int(SUB / 256);
+            uint4 keep[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                keep[i] = acc[i];
+#pragma unroll
+            for (int i = 0; i + R < DEC_T; ++i)
+                acc[i] = acc[i + R];
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                acc[DEC_T - R + i] = keep[i];
         }
     }
 
@@ -378,7 +470,12 @@ extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const in
     const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
-    hipLaunchKernelGGL(k_decode_big, dim3(u32(grid)), dim3(256), 0, st, *g, work, status, u32(ngroups),
-                       u32(nslices ? nslices : 1));
+    const bool pal = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->parts) | g->part_pitch) & 15) == 0;
+    if (pal)
+        hipLaunchKernelGGL(k_decode_big<true>, dim3(u32(grid)), dim3(256), 0, st, *g, work, status, u32(ngroups),
+                           u32(nslices ? nslices : 1));
+    else
+        hipLaunchKernelGGL(k_decode_big<false>, dim3(u32(grid)), dim3(256), 0, st, *g, work, status, u32(ngroups),
+                           u32(nslices ? nslices : 1));
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -291,61 +291,76 @@ __global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *ava
                                                     int k, u8 *work, int32_t *status, const GfTables *gft)
 {
     __shared__ GfLds L;
-    __shared__ u8 x[256], slot[256], M[256];
-    __shared__ int have;
+    __shared__ u8 sid[256], sav[256], x[256], slot[256], M[2][260];
+    __shared__ u8 q[64][256];  // one column's quotient per thread
     gf_stage(L, gft);
     const u32 s = blockIdx.x;
+    const int tid = threadIdx.x;
     u8 *wk = work + u64(s) * u64(k + k * k);
-    if (threadIdx.x == 0) {
-        const u8 *sid = ids + u64(s) * n_slots;
-        const u8 *sav = avail + u64(s) * navail;
-        int h = 0;
-        for (int c = 0; c < navail && h < k; ++c) {
-            const u8 sl = sav[c];
-            const u8 id = sid[sl];
-            bool dup = false;
+    for (int i = tid; i < n_slots; i += 64)
+        sid[i] = ids[u64(s) * n_slots + i];
+    for (int i = tid; i < navail; i += 64)
+        sav[i] = avail[u64(s) * navail + i];
+    __syncthreads();
+    // first k offered slots with distinct ids, in offer order
+    // (crt/nk8.c:512-537): lane c keeps slot c unless an earlier offer has
+    // its id; a ballot prefix places the kept ones
+    int h = 0;
+    for (int base = 0; base < navail && h < k; base += 64) {
+        const int c = base + tid;
+        bool keep = false;
+        u8 id = 0, sl = 0;
+        if (c < navail) {
+            sl = sav[c];
+            id = sid[sl];
+            keep = true;
             for (int d = 0; d < c; ++d)
-                dup |= sid[sav[d]] == id;
-            if (dup)
-                continue;
-            x[h] = id;
-            slot[h] = sl;
-            ++h;
+                keep &= sid[sav[d]] != id;
         }
-        have = h;
-        if (status)
-            status[s] = h < k ? -EINVAL : 0;
-        if (h == k) {
-            // M(t) = prod_c (t + x_c), coefficients M[0..k]
-            M[0] = 1;
-            for (int c = 0; c < k; ++c) {
-                M[c + 1] = M[c];
-                for (int i = c; i >= 1; --i)
-                    M[i] = M[i - 1] ^ gf_mul(L, x[c], M[i]);
-                M[0] = gf_mul(L, x[c], M[0]);
-            }
+        const u64 bal = __ballot(keep);
+        const int pos = h + __popcll(bal & ((1ull << tid) - 1ull));
+        if (keep && pos < k) {
+            x[pos] = id;
+            slot[pos] = sl;
         }
+        h += __popcll(bal);
+    }
+    if (tid == 0 && status)
+        status[s] = h < k ? -EINVAL : 0;
+    if (h < k)
+        return;  // wave-uniform
+    // M(t) = prod_c (t + x_c), coefficients M[0..k]: k steps, lanes over
+    // the coefficients (double-buffered)
+    for (int i = tid; i <= k; i += 64) {
+        M[0][i] = i == 0 ? 1 : 0;
+        M[1][i] = 0;
     }
     __syncthreads();
-    if (have < k)
-        return;
-    for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    for (int c = 0; c < k; ++c) {
+        const int cur = c & 1;
+        for (int i = tid; i <= c + 1; i += 64)
+            M[cur ^ 1][i] = (i ? M[cur][i - 1] : u8(0)) ^ gf_mul(L, x[c], M[cur][i]);
+        __syncthreads();
+    }
+    const u8 *Mk = M[k & 1];
+    for (int c = tid; c < k; c += 64) {
         wk[c] = slot[c];
-        u8 *row = wk + k + c * k;
+        u8 *qc = q[tid];
         const u8 xc = x[c];
-        // Q(t) = M(t) / (t + x_c), synthetic division from the top.
-        u8 q = M[k];
-        row[k - 1] = q;
+        // Q(t) = M(t) / (t + x_c), synthetic division from the top
+        u8 qq = Mk[k];
+        qc[k - 1] = qq;
         for (int i = k - 1; i >= 1; --i) {
-            q = M[i] ^ gf_mul(L, xc, q);
-            row[i - 1] = q;
+            qq = Mk[i] ^ gf_mul(L, xc, qq);
+            qc[i - 1] = qq;
         }
         // D = Q(x_c) = prod_{c' != c} (x_c + x_c')
         u8 d = 0;
         for (int i = k - 1; i >= 0; --i)
-            d = gf_mul(L, d, xc) ^ row[i];
+            d = gf_mul(L, d, xc) ^ qc[i];
+        u8 *row = wk + k + c * k;
         for (int i = 0; i < k; ++i)
-            row[i] = gf_div(L, row[i], d);
+            row[i] = gf_div(L, qc[i], d);
     }
 }
 
