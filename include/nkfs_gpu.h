@@ -57,10 +57,14 @@ int nkfs_gpu_get_devices(int *devices, int max);
  * starts with the measured defaults; tools and tests replace
  * them with nkfs_tune_set to compare kernels in one process.  The launchers
  * read only this struct: no environment variable changes what runs. */
-/* NKFS_ENC_WIDE: part-group encoder (any n, k <= 16; the default beyond the
- * fused kernels' n <= 8, k <= 8); NKFS_ENC_GENERIC: thread-per-row kernel;
- * NKFS_ENC_BIG: column-chunked encoder (any k; the default for k > 16) */
-enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG };
+/* NKFS_ENC_WIDE: part-group encoder + a second XXH64 pass (any n, k <= 16;
+ * the default beyond the fused kernels' n <= 8, k <= 8 for batches too small
+ * to fill the chip); NKFS_ENC_WIDE_WS: part-group encoder with XXH64 fused
+ * (a hash wave per workgroup; the default for k <= 16 batches that fill the
+ * chip); NKFS_ENC_GENERIC: thread-per-row kernel; NKFS_ENC_BIG:
+ * column-chunked encoder (any k; the default for k > 16) */
+enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG,
+       NKFS_ENC_WIDE_WS };
 /* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16);
  * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16) */
 enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG };

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                     e.w ^= tv.w;
                 }
                 acc[t] = e;
-                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
                 xc = xn;
                 x4c = x4n;
                 posc = posn;
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
                     e.w ^= tv.w;
                 }
                 acc[t] = e;
-                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x));
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
             }
             constexpr int R = int(SUB / 256);
             uint4 keep[R];

@@ -596,6 +596,7 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,
                                 int cus, hipStream_t st);
 extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st);
+extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st);
 extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const void *gf, hipStream_t st);
 extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
@@ -661,15 +662,25 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     int rc = -ENOSYS;
     const int kern = nkfs_tune_now().enc_kernel;
     if (g->n <= 8 && g->k <= 8 && kern != NKFS_ENC_GENERIC && kern != NKFS_ENC_WIDE && kern != NKFS_ENC_BIG &&
-        !few_big_stripes(g)) {
+        kern != NKFS_ENC_WIDE_WS && !few_big_stripes(g)) {
         rc = with_size_order(g, st, [&](const nkfs_geom *go) { return fast_encode(go, ids, digests, st); });
         if (rc == -ENOSYS)
             rc = fast_encode(g, ids, digests, st);
     }
     if (rc != -ENOSYS)
         return rc;
-    // n > 8 (or a few big stripes): part groups of 8 for k <= 16, 16-column
-    // chunks beyond (nk8_big.hip), then the batched XXH64 of the parts
+    // n > 8 (or a few big stripes), k <= 16: with digests and a batch that
+    // fills the chip (two workgroups of 16 parts per CU), the part-group
+    // encoder with XXH64 fused (nk8_wide.hip, k_encode_wide_ws)
+    if (digests && g->k <= 16 &&
+        (kern == NKFS_ENC_WIDE_WS ||
+         (kern == NKFS_ENC_AUTO && u64(g->nstripes) * u64((g->n + 15) / 16) >= 2u * u64(nkfs_cu_count())))) {
+        rc = nkfs_wide_ws_encode(g, ids, digests, st);
+        if (rc != -ENOSYS)
+            return rc;
+    }
+    // else part groups of 8 for k <= 16, 16-column chunks beyond
+    // (nk8_big.hip), then the batched XXH64 of the parts
     if (kern != NKFS_ENC_GENERIC) {
         rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
         if (rc == -ENOSYS)

@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "nk8_dev.h"
+#include "xxh64_dev.h"
 
 using namespace nkfs;
 using namespace nkfs::dev;
@@ -163,6 +164,203 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
                 }
             }
         }
+    }
+}
+
+// Fused encode + XXH64 for the part-group shapes (2 <= k <= 16, any n):
+// a workgroup = (stripe, group of 16 parts) walks the stripe's rows in
+// order with NE encoder waves and one hash wave.  Encoder lane = 4
+// consecutive rows per chunk (k dwords of the block; CR = 256 NE rows per
+// chunk): the packed tables T_m[x] = (x_{16g}^m x, ..., x_{16g+15}^m x),
+// 16-byte entries, give a row's term for all 16 parts per ds_read_b128;
+// 4 rows x 16 parts are transposed into one dword of 4 rows per part, stored
+// to HBM (a wave writes 256 contiguous bytes of a part per instruction) and
+// into an LDS exchange.  The hash wave (lane = 4 part + a) copies chunk c's
+// words to registers and folds them while the encoders produce chunk c+1
+// (two barriers per chunk): XXH64 is serial over a
+// part's rows (crt/xxhash.c:791-810), so a stripe must be walked in order by
+// one workgroup, and the parts are never read back (the two-pass form
+// re-read them: W1 PMC traffic 1.57x).  The group workgroups of a stripe
+// sit on one XCD (b mod 8) and share its block's lines in L2.
+template <int K, int NE>
+__global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g, const u8 *ids, u64 *digests,
+                                                                  u32 ngroups)
+{
+    constexpr int CR = 256 * NE;   // rows per chunk
+    constexpr int SP = CR + 32;    // exchange bytes per part (+32: the hash lanes' reads spread over the banks)
+    constexpr int TB = 256 * 16;   // bytes per packed table
+    constexpr int RPC = CR / 32;   // XXH64 rounds per chain per chunk
+    __shared__ __attribute__((aligned(16))) u8 tbl[(K - 1) * TB];
+    // single-buffered exchange: two barriers per chunk (the hash wave copies
+    // its words to registers between them); double-buffered, a workgroup
+    // needs 79 KiB at k = 12 and the CU keeps only one resident
+    __shared__ __attribute__((aligned(16))) u8 xbuf[16 * SP];
+
+    const u32 b = blockIdx.x;
+    const u32 grp = (b >> 3) % ngroups;
+    const u32 s = (b >> 3) / ngroups * 8 + (b & 7);
+    if (s >= g.nstripes)
+        return;  // the whole workgroup
+    const Stripe v = stripe_at(g, s);
+    const int n = g.n;
+    const int p0 = int(grp) * 16, np = min(16, n - p0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const u32 nch = (v.ps + CR - 1) / CR;
+    if (!nch)
+        return;
+
+    if (wave < NE) {
+        // ------------------------------------------------------ encoder wave
+        const u32 rbase = u32(wave) * 256u + 4u * u32(lane);  // this lane's first row in every chunk
+        const bool aligned =
+            ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
+        u32 d[K];  // 4 rows x K bytes
+        auto load_task = [&](u32 r0) {
+            const u64 off = u64(r0) * K;
+            if (aligned && off + 4 * K <= v.B) {
+                const u32 *src = reinterpret_cast<const u32 *>(v.blk + off);
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    d[q] = src[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    u32 x = 0;
+                    for (int e = 0; e < 4; ++e) {
+                        const u64 p = off + 4 * q + e;
+                        if (p < v.B)
+                            x |= u32(v.blk[p]) << (8 * e);
+                    }
+                    d[q] = x;
+                }
+            }
+        };
+        if (rbase < v.ps)
+            load_task(rbase);  // first chunk requested before the table build
+        // tables T_m, m = 1..K-1, of the group's parts, split over the
+        // encoder waves (coefficient 0 past n: nothing is stored for those)
+        u32 idw[4] = {0, 0, 0, 0};
+        for (int e = 0; e < np; ++e)
+            idw[e >> 2] |= u32(ids[u64(s) * u64(n) + u64(p0 + e)]) << (8 * (e & 3));
+        u32 coef[4] = {idw[0], idw[1], idw[2], idw[3]};
+#pragma unroll 1
+        for (int m = 1; m < K; ++m) {
+            if ((m - 1) % NE == wave) {
+                u32 basis[8][4];
+                make_basis<4>(basis, coef);
+                build_table16(tbl + (m - 1) * TB, basis, lane);
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                coef[w] = gf_mul_packed(coef[w], idw[w]);
+        }
+        __syncthreads();
+
+        for (u32 c = 0; c < nch; ++c) {
+            const u32 r0 = c * CR + rbase;
+            if (r0 < v.ps) {
+                // rows r0..r0+3: the m = 0 term is the byte itself (x^0 = 1)
+                u32 rows[4][4];
+                u32 tdep = 0;  // 0 at run time: one row's lookups in flight at a time
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int pb = rr * K;
+                    const u32 rep = __builtin_amdgcn_perm(0u, d[pb >> 2], 0x01010101u * u32(pb & 3));
+                    uint4 e = make_uint4(rep, rep, rep, rep);
+#pragma unroll
+                    for (int m = 1; m < K; ++m) {
+                        const int p = pb + m;
+                        const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                        const uint4 t = *reinterpret_cast<const uint4 *>(tbl + tdep + (m - 1) * TB + byte * 16);
+                        e.x ^= t.x;
+                        e.y ^= t.y;
+                        e.z ^= t.z;
+                        e.w ^= t.w;
+                    }
+                    rows[rr][0] = e.x;
+                    rows[rr][1] = e.y;
+                    rows[rr][2] = e.z;
+                    rows[rr][3] = e.w;
+                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
+                }
+                if (r0 + CR < v.ps)
+                    load_task(r0 + CR);  // next chunk's rows in flight under this chunk's stores
+                // 4 rows x 16 parts -> 16 parts x 4 rows (one dword each)
+                u32 out[16];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    transpose4(rows[0][w], rows[1][w], rows[2][w], rows[3][w], out[4 * w], out[4 * w + 1],
+                               out[4 * w + 2], out[4 * w + 3]);
+                u8 *xb = xbuf + rbase;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i < np) {
+                        u8 *dst = v.parts + u64(p0 + i) * v.pitch + r0;
+                        if (aligned && r0 + 4 <= v.ps) {
+                            *reinterpret_cast<u32 *>(dst) = out[i];
+                        } else {
+                            for (u32 e = 0; e < 4 && r0 + e < v.ps; ++e)
+                                dst[e] = u8(out[i] >> (8 * e));
+                        }
+                        *reinterpret_cast<u32 *>(xb + i * SP) = out[i];
+                    }
+                }
+            }
+            __syncthreads();  // chunk c is in the exchange
+            __syncthreads();  // the hash wave has copied it
+        }
+        return;
+    }
+
+    // ---------------------------------------------------------------- hash wave
+    const int hi = lane >> 2, ha = lane & 3;  // part p0 + hi, accumulator ha
+    const bool hlane = hi < np;
+    const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
+    u64 acc = xxh_acc_init(ha, 0);
+    const int xoff = hi * SP + 8 * ha;
+    static_assert(RPC <= 32, "hash words staged in registers");
+    __syncthreads();  // tables built
+    u64 tw[4] = {0, 0, 0, 0};  // the tail words of the last chunk (read before it is overwritten)
+    const u32 left = v.ps & 31;
+    for (u32 c = 0; c < nch; ++c) {
+        __syncthreads();  // chunk c is in the exchange
+        u64 hw[RPC];
+        int hv = 0;
+        if (hlane) {
+            const u8 *src = xbuf + xoff;
+            const int lft = int(nst) - int(c * RPC);
+            hv = lft < 0 ? 0 : (lft > RPC ? RPC : lft);
+#pragma unroll
+            for (int r = 0; r < RPC; ++r)
+                hw[r] = *reinterpret_cast<const u64 *>(src + 32 * r);
+            if (c == nch - 1 && left) {
+                const u8 *t = xbuf + hi * SP + (nst * 32 - c * CR);
+#pragma unroll
+                for (u32 e = 0; e < 32; ++e)
+                    if (e < left)
+                        tw[e >> 3] |= u64(t[e]) << (8 * (e & 7));
+            }
+        }
+        __syncthreads();  // the encoders may overwrite it now
+        if (hv == RPC) {
+#pragma unroll
+            for (int r = 0; r < RPC; ++r)
+                acc = xxh_round(acc, hw[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPC; ++r) {
+                const u64 nx = xxh_round(acc, hw[r]);
+                acc = r < hv ? nx : acc;
+            }
+        }
+    }
+    const int base = lane & ~3;
+    const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+    const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+    if (hlane && ha == 0) {
+        u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+        h += v.ps;
+        digests[u64(s) * u64(n) + u64(p0 + hi)] = xxh_tail_regs(h, tw, left);
     }
 }
 
@@ -352,6 +550,53 @@ extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus,
         NKFS_K(14)
         NKFS_K(15)
         NKFS_K(16)
+#undef NKFS_K
+    default:
+        return -ENOSYS;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// Fused encode + XXH64 of every part, 2 <= k <= 16, any n <= 255: one
+// workgroup per (stripe, group of 16 parts) walking the stripe in order.
+// For batches that fill the chip (the caller decides); -ENOSYS outside the
+// shapes.
+extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st)
+{
+    const int k = g->k;
+    if (k < 2 || k > WIDE_MAX_K || g->n < k || g->n > 255 || !digests)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    const u64 ngroups = (u64(g->n) + 15) / 16;
+    const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups;
+    if (grid > 0x7FFFFFFFull)
+        return -EINVAL;
+    const dim3 gd = dim3(u32(grid));
+    switch (k) {
+#define NKFS_K(KK, NE)                                                                                    \
+    case KK:                                                                                              \
+        hipLaunchKernelGGL((k_encode_wide_ws<KK, NE>), gd, dim3(64 * (NE + 1)), 0, st, *g, ids, digests,  \
+                           u32(ngroups));                                                                 \
+        break;
+        // three encoder waves + the hash wave = 256 threads: a 320-thread
+        // workgroup (four encoder waves) stayed alone on its CU (SQ: ~5
+        // resident waves per CU) whatever its LDS and VGPRs
+        NKFS_K(2, 3)
+        NKFS_K(3, 3)
+        NKFS_K(4, 3)
+        NKFS_K(5, 3)
+        NKFS_K(6, 3)
+        NKFS_K(7, 3)
+        NKFS_K(8, 3)
+        NKFS_K(9, 3)
+        NKFS_K(10, 3)
+        NKFS_K(11, 3)
+        NKFS_K(12, 3)
+        NKFS_K(13, 3)
+        NKFS_K(14, 3)
+        NKFS_K(15, 3)
+        NKFS_K(16, 3)
 #undef NKFS_K
     default:
         return -ENOSYS;

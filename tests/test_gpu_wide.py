@@ -1,5 +1,7 @@
-"""GPU parity of the part-group encoder (nk8_wide.hip, NKFS_ENC_WIDE): the
-default for n > 8 with k <= 16 and for a handful of big stripes.
+"""GPU parity of the part-group encoders (nk8_wide.hip): NKFS_ENC_WIDE (row
+slices + a second XXH64 pass; for a handful of big stripes) and
+NKFS_ENC_WIDE_WS (XXH64 fused by a hash wave; the default for n > 8 or k > 8
+with k <= 16 on batches that fill the chip).
 
 Every case is checked bit-exact against the thread-per-row general kernel
 (NKFS_ENC_GENERIC) on all stripes and against the oracle's parts and XXH64
@@ -72,12 +74,15 @@ def test_wide_encode_matches(L, O, n, k, B, S):
     with _tuned(enc_kernel=_enc("wide")):
         p1, d1 = batch.encode(blocks, B, n, k, ids)
         p2, _ = batch.encode(blocks, B, n, k, ids, digests=False)
+    with _tuned(enc_kernel=_enc("wide_ws")):  # XXH64 fused (hash wave)
+        p4, d4 = batch.encode(blocks, B, n, k, ids)
     p3, d3 = batch.encode(blocks, B, n, k, ids)  # default dispatch
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
     assert torch.equal(p0[:, :ps], p2[:, :ps])
     assert torch.equal(p0[:, :ps], p3[:, :ps]) and torch.equal(d0, d3)
+    assert torch.equal(p0[:, :ps], p4[:, :ps]) and torch.equal(d0, d4)
     got = [u64(x) for x in d1.cpu().tolist()]
     for s in sorted({0, S // 2, S - 1}):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
@@ -104,7 +109,7 @@ def test_wide_encode_ragged(L, O, n, k, gap):
         host[boff[s]: boff[s] + B] = synth.stripe_bytes(700 + s, int(B))
     ids_np = synth.batch_ids(len(sizes), n, first=700)
     outs = []
-    for kern in ("generic", "wide"):
+    for kern in ("generic", "wide", "wide_ws"):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
         with _tuned(enc_kernel=_enc(kern)):
@@ -113,6 +118,7 @@ def test_wide_encode_ragged(L, O, n, k, gap):
         torch.cuda.synchronize()
         outs.append((parts.cpu().numpy(), [u64(x) for x in dig.cpu().tolist()]))
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    assert np.array_equal(outs[0][0], outs[2][0]) and outs[0][1] == outs[2][1]
     pn, got = outs[1]
     for s in (0, 2, 3, 4, len(sizes) - 1):
         B = int(sizes[s])
@@ -189,3 +195,25 @@ def test_wide_decode_matches(L, O, n, k, B, S):
     pn = parts[s * n:(s + 1) * n, :batch.part_size(B, k)].cpu().numpy()
     got = O.decode([pn[j] for j in sel], [int(ids_np[s, j]) for j in sel], k, B)
     assert np.array_equal(np.asarray(got), ref[s].numpy())
+
+
+@pytest.mark.parametrize("n,k,B,S", [(16, 12, 1048576, 600), (20, 16, 65536, 700), (12, 9, 4099, 2000)])
+def test_wide_ws_default_dispatch_against_oracle(L, O, n, k, B, S):
+    """Batches that fill the chip take the fused part-group encoder by
+    default: parts and XXH64 against the oracle on a sample of stripes, and
+    against the two-pass form on all of them."""
+    from nkfs_amd import batch
+    blocks = batch.synth(S, B, first=77 + k)
+    ids_np = synth.batch_ids(S, n, first=77 + k)
+    ids = dev(ids_np)
+    p1, d1 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("wide")):
+        p0, d0 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    ps = batch.part_size(B, k)
+    assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    got = [u64(x) for x in d1.cpu().tolist()]
+    for s in sorted({0, S // 3, S - 1}):
+        want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
+        assert np.array_equal(p1[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), s
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
