@@ -445,6 +445,8 @@ __global__ __launch_bounds__(64) void k_verify_generic(nkfs_geom g, int n_slots,
 // grid's tail).  One workgroup bucket-sorts the stripes by part size into
 // perm (256 buckets: 8 per octave, largest first).  The order inside a
 // bucket depends on atomics; it changes timing only, never an output.
+constexpr u32 ORDER_MAXP = 60;  // stripes per thread of k_order_by_size (LDS bytes)
+
 __device__ inline u32 size_bucket(u32 B, int k)
 {
     const u32 ps = part_size_of(B, k);
@@ -457,25 +459,70 @@ __device__ inline u32 size_bucket(u32 B, int k)
 
 __global__ __launch_bounds__(1024) void k_order_by_size(const u32 *sizes, u32 count, int k, u32 *perm)
 {
+    // thread t takes positions t, t + 1024, ... (at most ORDER_MAXP: the
+    // launcher caps count); the buckets are computed once, all loads
+    // independent, into LDS bytes, then counted and placed with
+    // wave-aggregated LDS atomics (one per distinct bucket in a wave: a few
+    // size classes would otherwise serialise thousands of adds on one word)
     __shared__ u32 cnt[256];
+    __shared__ u8 bks[ORDER_MAXP * 1024];
     const u32 t = threadIdx.x;
     if (t < 256)
         cnt[t] = 0;
-    __syncthreads();
-    for (u32 i = t; i < count; i += blockDim.x)
-        atomicAdd(&cnt[size_bucket(sizes[i], k)], 1u);
-    __syncthreads();
-    if (t == 0) {
-        u32 run = 0;
-        for (int b = 0; b < 256; ++b) {
-            const u32 c = cnt[b];
-            cnt[b] = run;
-            run += c;
-        }
+    const u32 rounds = (count + 1023) / 1024;
+#pragma unroll 4
+    for (u32 j = 0; j < rounds; ++j) {
+        const u32 i = t + 1024u * j;
+        bks[i] = u8(i < count ? size_bucket(sizes[i < count ? i : 0], k) : 0u);
     }
     __syncthreads();
-    for (u32 i = t; i < count; i += blockDim.x)
-        perm[atomicAdd(&cnt[size_bucket(sizes[i], k)], 1u)] = i;
+    const u64 lt = (1ull << (t & 63)) - 1ull;
+    auto rank = [&](u32 bk, bool live) -> u32 {
+        u64 todo = __ballot(live);
+        u32 pos = 0;
+        while (todo) {
+            const int leader = __builtin_ctzll(todo);
+            const u32 lb = __shfl(bk, leader, 64);
+            const u64 same = __ballot(live && bk == lb);
+            u32 base = 0;
+            if (int(t & 63) == leader)
+                base = atomicAdd(&cnt[lb], u32(__popcll(same)));
+            base = __shfl(base, leader, 64);
+            if (live && bk == lb)
+                pos = base + u32(__popcll(same & lt));
+            todo &= ~same;
+        }
+        return pos;
+    };
+#pragma unroll 1
+    for (u32 j = 0; j < rounds; ++j) {
+        const u32 i = t + 1024u * j;
+        (void)rank(bks[i], i < count);
+    }
+    __syncthreads();
+    if (t < 64) {  // exclusive prefix over the 256 counters: 4 per lane
+        const u32 c0 = cnt[4 * t], c1 = cnt[4 * t + 1], c2 = cnt[4 * t + 2], c3 = cnt[4 * t + 3];
+        u32 s = c0 + c1 + c2 + c3, x = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(x, d, 64);
+            if (int(t) >= d)
+                x += y;
+        }
+        x -= s;
+        cnt[4 * t] = x;
+        cnt[4 * t + 1] = x + c0;
+        cnt[4 * t + 2] = x + c0 + c1;
+        cnt[4 * t + 3] = x + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (u32 j = 0; j < rounds; ++j) {
+        const u32 i = t + 1024u * j;
+        const u32 pos = rank(bks[i], i < count);
+        if (i < count)
+            perm[pos] = i;
+    }
 }
 
 // ---------------------------------------------------------- synthetic
@@ -578,8 +625,8 @@ extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
 template <class F>
 static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 {
-    if (!g->block_sizes || g->order || !nkfs_tune_now().size_order)
-        return -ENOSYS;
+    if (!g->block_sizes || g->order || !nkfs_tune_now().size_order || g->nstripes > ORDER_MAXP * 1024u)
+        return -ENOSYS;  // (k_order_by_size: ORDER_MAXP stripes per thread)
     u32 *perm = nullptr;
     if (hipMallocAsync(reinterpret_cast<void **>(&perm), size_t(g->nstripes) * sizeof(u32), st) != hipSuccess)
         return -ENOSYS;

@@ -781,17 +781,27 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
 __global__ __launch_bounds__(1024) void k_slice_scan(const u32 *sizes, const u32 *order, u32 nstripes, int k,
                                                      u32 rows, u32 *sfirst, u32 *stotal)
 {
+    // thread t owns the contiguous positions [t*per, t*per + per); the
+    // per-stripe slice counts are loaded once, all independently (clamped
+    // indices, no branch), and kept in registers for the prefix pass
+    constexpr int MAXP = 64;  // the launcher keeps nstripes <= 64 * 1024
     __shared__ u32 part[1024];
     const u32 t = threadIdx.x;
     const u32 per = (nstripes + 1023) / 1024;
-    const u32 a = min(nstripes, t * per), b = min(nstripes, a + per);
-    auto slices_of = [&](u32 p) {
-        const u32 ps = part_size_of(sizes[order ? order[p] : p], k);
-        return ps ? (ps + rows - 1) / rows : 1u;  // an empty stripe is one (empty) pass
-    };
+    const u32 a = t * per;
+    u32 cnt[MAXP];
     u32 sum = 0;
-    for (u32 p = a; p < b; ++p)
-        sum += slices_of(p);
+#pragma unroll
+    for (int j = 0; j < MAXP; ++j) {
+        const u32 p = a + u32(j);
+        const bool live = u32(j) < per && p < nstripes;
+        const u32 pc = live ? p : 0u;
+        const u32 sz = sizes[order ? order[pc] : pc];
+        const u32 ps = part_size_of(sz, k);
+        const u32 c = ps ? (ps + rows - 1) / rows : 1u;  // an empty stripe is one (empty) pass
+        cnt[j] = live ? c : 0u;
+        sum += cnt[j];
+    }
     part[t] = sum;
     __syncthreads();
     for (u32 d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
@@ -801,9 +811,12 @@ __global__ __launch_bounds__(1024) void k_slice_scan(const u32 *sizes, const u32
         __syncthreads();
     }
     u32 run = t ? part[t - 1] : 0u;
-    for (u32 p = a; p < b; ++p) {
-        sfirst[p] = run;
-        run += slices_of(p);
+#pragma unroll
+    for (int j = 0; j < MAXP; ++j) {
+        const u32 p = a + u32(j);
+        if (u32(j) < per && p < nstripes)
+            sfirst[p] = run;
+        run += cnt[j];
     }
     if (t == 1023) {
         sfirst[nstripes] = part[1023];
@@ -948,7 +961,8 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
                                  int navail, void *work, int32_t *status, const void *gf, int units, int waves,
                                  int cus, hipStream_t st)
 {
-    if (g->k > 8 || (reinterpret_cast<uintptr_t>(g->parts) & 15) || (!g->block_sizes && (g->part_pitch & 15)))
+    if (g->k > 8 || (reinterpret_cast<uintptr_t>(g->parts) & 15) || (!g->block_sizes && (g->part_pitch & 15)) ||
+        (g->block_sizes && g->nstripes > 64u * 1024u))  // k_slice_scan: 64 stripes per thread
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
