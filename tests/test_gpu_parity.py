@@ -786,6 +786,44 @@ def test_ragged_slice_decode_matches_wave(L, n, k, units):
             assert st[s] == 0 and np.array_equal(o[boff[s]: boff[s] + B].numpy(), host[boff[s]: boff[s] + B]), s
 
 
+@pytest.mark.parametrize("n,k,units", [(8, 5, 2), (6, 4, 4)])
+def test_ragged_slice_decode_past_2gib(L, n, k, units):
+    """The ragged slice decoder's persistent grid over more slices than it has
+    waves (every wave walks several slices, with the next slice's descriptor
+    prefetched) and with block and part offsets past 2^31 (64-bit offsets
+    carried through the prefetch): encode -> erase n-k -> decode round trip,
+    bit-exact, and the same bytes as the wave decoder (crt/nk8.c:446-599)."""
+    from nkfs_amd import batch
+    base = (1 << 31) + 4096
+    sizes = np.array([1048576] * 28 + [4096, 65536, 777, 1048575] * 3, np.uint32)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, 0, first_off=base)
+    poff = poff + base
+    host = np.zeros(pos - base, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s] - base: boff[s] - base + B] = synth.stripe_bytes(900 + s, int(B))
+    blocks = torch.zeros(pos, dtype=torch.uint8, device="cuda")
+    blocks[base:] = dev(host)
+    ids_np = synth.batch_ids(len(sizes), n, first=900)
+    parts = torch.zeros(base + ppos, dtype=torch.uint8, device="cuda")
+    sz = dev(sizes.astype(np.int32))
+    batch.encode_ragged(blocks, dev(boff), sz, n, k, dev(ids_np), parts, dev(poff), None, int(sizes.max()))
+    avail = synth.batch_survivors(len(sizes), n, k, first=900)
+    res = []
+    for kern in ("slice", "wave"):
+        with _tuned(dec_kernel=_dec(kern), dec_units=units):
+            out = torch.zeros(pos, dtype=torch.uint8, device="cuda")
+            st = batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(avail), k, out, dev(boff), sz,
+                                     int(sizes.max()))
+            torch.cuda.synchronize()
+            assert int(st.abs().sum()) == 0
+            res.append(out[base:].cpu())
+            del out
+    assert torch.equal(res[0], res[1])
+    assert np.array_equal(res[0].numpy(), host)
+    del parts, blocks
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("S,B", [(512, 1048576), (1024, 1048576), (512, 262144)])
 def test_bench_kernels_against_oracle(L, O, S, B):
     """The kernels the bench times, pinned through struct nkfs_tune and
