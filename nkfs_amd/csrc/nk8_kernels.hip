@@ -609,7 +609,7 @@ extern "C" size_t nkfs_gf_tables_bytes(void) { return sizeof(GfTables); }
 
 extern "C" uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k)
 {
-    return u64(nstripes) * NKFS_PLAN_STRIDE(k);
+    return u64(nstripes) * u64(k + k * k);
 }
 
 extern "C" int nkfs_launch_gf_init(void *gf, void *stream)

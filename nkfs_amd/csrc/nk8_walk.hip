@@ -80,9 +80,6 @@ Shape occupancy_shape(const void *kern, int target)
     return sh;
 }
 
-// NKFS_PLAN_STRIDE as a constant expression
-__host__ __device__ constexpr int plan_stride(int k) { return (k + k * k + 3) & ~3; }
-
 u32 part_size_of_host(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -524,7 +521,7 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
         return;
     const u8 *sid = ids + u64(s) * n_slots;
     const u8 *sav = avail + u64(s) * navail;
-    u8 *pl = plan + u64(s) * plan_stride(K);
+    u8 *pl = plan + u64(s) * (K + K * K);
     u32 x[K], sl[K];
     int h = 0;
     for (int c = 0; c < navail && h < K; ++c) {
@@ -582,59 +579,63 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
     }
 }
 
-// What one slice needs before its first part load: the stripe, the slice,
-// its block size and offsets, and the stripe's plan (K slots then the K x K
-// inverse, as plan words).  The ragged decoder loads the NEXT slice's
-// descriptor while it works on this one, so the chain smap -> sizes/offsets
-// -> plan -> parts costs one hop per slice instead of three.
-template <int K>
-struct SliceMeta {
-    static constexpr int PLW = plan_stride(K) / 4;
-    u32 s, slice, B;
-    u64 poff, boff;
-    u32 pw[PLW];
-};
-
-template <int K>
-__device__ __forceinline__ u32 plan_byte(const SliceMeta<K> &m, int i)
-{
-    return (m.pw[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-}
-
-template <int K>
-__device__ __forceinline__ void load_plan(SliceMeta<K> &m, const u8 *plan)
-{
-    const u32 *pp = reinterpret_cast<const u32 *>(plan + u64(m.s) * plan_stride(K));
-#pragma unroll
-    for (int i = 0; i < SliceMeta<K>::PLW; ++i)
-        m.pw[i] = pp[i];
-}
-
-// One slice: rows [slice*R, slice*R + R) of one stripe, R = 1024*U.
+// One-shot slice: rows [slice*R, slice*R + R) of one stripe, R = 1024*U.
 // XPOSE: output rows go through LDS so every store instruction writes one
 // contiguous 1 KiB run (lane l owns 16 rows = 16K contiguous bytes; stored
-// directly that is a 16K-byte lane stride).  PAL: the stripe's parts are
-// 16-byte aligned (ragged part offsets are caller data; uniform batches are
-// checked by the launcher).
-template <int K, int E, int U, bool XPOSE, bool RAGGED, bool PAL>
-__device__ __forceinline__ void slice_body(const nkfs_geom &g, const SliceMeta<K> &m, u8 *tbl, u8 *obuf, int li)
+// directly that is a 16K-byte lane stride).
+// RAGGED: a persistent grid walks the (stripe, slice) list of a ragged
+// batch -- smap[w] = (processing position << 32) | slice of slice w (g.order
+// applied; k_slice_scan + k_slice_map), *stotal = all slices -- and each
+// slice is one pass of the same one-shot body.
+template <int K, int E, int U, bool XPOSE, bool RAGGED>
+__global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, const u8 *plan, u32 slices,
+                                                     const u64 *smap, const u32 *stotal)
 {
     constexpr int W = E / 4;
     constexpr int TB = 256 * E;
     constexpr int R = 1024 * U;
     constexpr int LS = 16 * K + (K % 2 == 0 ? 16 : 0);  // transpose bytes per lane (even K padded: bank spread)
-    const u32 B = m.B;
+    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
+    __shared__ __attribute__((aligned(16))) u8 obuf[XPOSE ? 64 * LS : 16];
+
+    const int li = threadIdx.x;
+    const u32 total = RAGGED ? *stotal : 0u;
+    for (u32 w = blockIdx.x;; w += gridDim.x) {
+    u32 s, slice;
+    if constexpr (RAGGED) {
+        if (w >= total)
+            return;
+        const u64 e = smap[w];
+        slice = u32(e);
+        s = g.order ? g.order[u32(e >> 32)] : u32(e >> 32);
+    } else {
+        s = w / slices;
+        slice = w % slices;
+        if (s >= g.nstripes)
+            return;
+    }
+    const u8 *pl = plan + u64(s) * (K + K * K);
+    const u32 sl0 = pl[0];
+    if (sl0 == 0xFF) {  // fewer than K distinct ids: status says -EINVAL, block untouched
+        if constexpr (RAGGED)
+            continue;
+        return;
+    }
+    const u32 B = RAGGED ? g.block_sizes[s] : g.block_size;
     const u32 ps = part_size_of(B, K);
     const u64 ppitch = RAGGED ? (u64(ps) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1) : g.part_pitch;
-    const u32 rbase = m.slice * R;
-    const u8 *pbase = g.parts + m.poff;
-    u8 *out = const_cast<u8 *>(g.blocks) + m.boff;
+    const u32 rbase = slice * R;
+    const u8 *pbase = RAGGED ? g.parts + g.part_off[s] : g.parts + u64(s) * n_slots * g.part_pitch;
+    u8 *out = const_cast<u8 *>(g.blocks) + (RAGGED ? g.block_off[s] : u64(s) * g.block_pitch);
+    // ragged part offsets are caller data: byte loads where a stripe's parts
+    // are not 16-byte aligned (uniform batches are checked by the launcher)
+    const bool pal = !RAGGED || (reinterpret_cast<uintptr_t>(pbase) & 15) == 0;
 
     // loads first (their latency hides under the table build)
     const u8 *src[K];
 #pragma unroll
     for (int c = 0; c < K; ++c)
-        src[c] = pbase + u64(plan_byte(m, c)) * ppitch;
+        src[c] = pbase + u64(c ? pl[c] : sl0) * ppitch;
     u32 pv[U][K][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -642,7 +643,7 @@ __device__ __forceinline__ void slice_body(const nkfs_geom &g, const SliceMeta<K
         if (r0 < ps)
 #pragma unroll
             for (int c = 0; c < K; ++c) {
-                if constexpr (PAL) {
+                if (pal) {
                     const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
                     pv[u][c][0] = t.x;
                     pv[u][c][1] = t.y;
@@ -652,7 +653,6 @@ __device__ __forceinline__ void slice_body(const nkfs_geom &g, const SliceMeta<K
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         u32 x = 0;
-#pragma unroll
                         for (int e = 0; e < 4; ++e)
                             x |= u32(src[c][r0 + 4 * q + e]) << (8 * e);  // within the pitch
                         pv[u][c][q] = x;
@@ -670,7 +670,7 @@ __device__ __forceinline__ void slice_body(const nkfs_geom &g, const SliceMeta<K
 #pragma unroll
             for (int b = 0; b < 4; ++b)
                 if (4 * w + b < K)
-                    x |= plan_byte(m, K + c * K + 4 * w + b) << (8 * b);
+                    x |= u32(pl[K + c * K + 4 * w + b]) << (8 * b);
             rw[w] = x;
         }
         u32 basis[8][W];
@@ -769,95 +769,9 @@ __device__ __forceinline__ void slice_body(const nkfs_geom &g, const SliceMeta<K
             }
         }
     }
-}
-
-// Uniform: one-shot wave per (stripe, slice).  RAGGED: a persistent grid
-// walks the slice list of a ragged batch -- smap[w] = (stripe << 32) | slice
-// (g.order already applied; k_slice_scan + k_slice_map), *stotal = all
-// slices -- loading slice w + grid's descriptor and slice w + 2*grid's map
-// entry before slice w's part loads (clamped indices: no branch), so they
-// land under slice w's work.
-template <int K, int E, int U, bool XPOSE, bool RAGGED>
-__global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, const u8 *plan, u32 slices,
-                                                     const u64 *smap, const u32 *stotal)
-{
-    __shared__ __attribute__((aligned(16))) u8 tbl[K * 256 * E];
-    __shared__ __attribute__((aligned(16))) u8 obuf[XPOSE ? 64 * (16 * K + (K % 2 == 0 ? 16 : 0)) : 16];
-    const int li = threadIdx.x;
-    SliceMeta<K> m;
-    if constexpr (!RAGGED) {
-        const u32 w = blockIdx.x;
-        m.s = w / slices;
-        m.slice = w % slices;
-        if (m.s >= g.nstripes)
-            return;
-        load_plan(m, plan);
-        if (plan_byte(m, 0) == 0xFF)  // fewer than K distinct ids: status says -EINVAL, block untouched
-            return;
-        m.B = g.block_size;
-        m.poff = u64(m.s) * n_slots * g.part_pitch;
-        m.boff = u64(m.s) * g.block_pitch;
-        slice_body<K, E, U, XPOSE, false, true>(g, m, tbl, obuf, li);
-    } else {
-        const u32 total = *stotal;
-        const u32 G = gridDim.x;
-        u32 w = blockIdx.x;
-        if (w >= total)
-            return;
-        // The prefetched words are loaded through an index the compiler
-        // cannot prove uniform (+ a zero it cannot see through), so they stay
-        // in VGPRs with their loads in flight until the next slice reads them
-        // (readfirstlane); uniform loads would be moved to SGPRs -- and
-        // waited for -- right after they issue.
-        u32 vz;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-        auto meta_of = [&](SliceMeta<K> &x, u64 e) {  // raw (VGPR) words
-            x.s = u32(e >> 32);
-            x.slice = u32(e);
-            const u32 si = x.s + vz;
-            x.B = g.block_sizes[si];
-            x.poff = g.part_off[si];
-            x.boff = g.block_off[si];
-            load_plan(x, plan + vz);
-        };
-        // (readfirstlane returns int: every word goes through u32 before it
-        // is widened, or a low word >= 2^31 sign-extends into the high one)
-        auto rfl = [](u32 v) { return u32(__builtin_amdgcn_readfirstlane(v)); };
-        auto uni = [&](const SliceMeta<K> &x) {
-            SliceMeta<K> y;
-            y.s = rfl(x.s);
-            y.slice = rfl(x.slice);
-            y.B = rfl(x.B);
-            y.poff = (u64(rfl(u32(x.poff >> 32))) << 32) | u64(rfl(u32(x.poff)));
-            y.boff = (u64(rfl(u32(x.boff >> 32))) << 32) | u64(rfl(u32(x.boff)));
-#pragma unroll
-            for (int i = 0; i < SliceMeta<K>::PLW; ++i)
-                y.pw[i] = rfl(x.pw[i]);
-            return y;
-        };
-        meta_of(m, smap[w + vz]);
-        u64 e_next = smap[(w + G < total ? w + G : total - 1) + vz];
-        for (;;) {
-            const bool more = w + G < total;
-            const SliceMeta<K> mu = uni(m);
-            meta_of(m, e_next);  // slice w + G, in flight under slice w
-            e_next = smap[(w + 2 * G < total ? w + 2 * G : total - 1) + vz];
-            if (plan_byte(mu, 0) != 0xFF) {
-                if ((reinterpret_cast<uintptr_t>(g.parts + mu.poff) & 15) == 0)
-                    slice_body<K, E, U, XPOSE, true, true>(g, mu, tbl, obuf, li);
-                else
-                    slice_body<K, E, U, XPOSE, true, false>(g, mu, tbl, obuf, li);
-                __syncthreads();  // the next slice rebuilds the tables
-            } else {
-                // vmcnt(0): slice_body's own waits retire the prefetch on the
-                // other path; without one here the compiler's count at the
-                // loop head is the worst of both, a full wait every slice
-                __builtin_amdgcn_s_waitcnt(0x0F70);
-            }
-            if (!more)
-                return;
-            w += G;
-        }
+    if constexpr (!RAGGED)
+        return;
+    __syncthreads();  // the next slice rebuilds the tables
     }
 }
 
@@ -910,18 +824,16 @@ __global__ __launch_bounds__(1024) void k_slice_scan(const u32 *sizes, const u32
     }
 }
 
-// smap[sfirst[p] + j] = (stripe << 32) | j for the slices j of the stripe at
-// processing position p (stripe = order[p], or p): one wave per stripe,
-// lanes over its slices.
-__global__ __launch_bounds__(256) void k_slice_map(const u32 *sfirst, const u32 *order, u32 nstripes, u64 *smap)
+// smap[sfirst[p] + j] = (p << 32) | j for the slices j of the stripe at
+// processing position p: one wave per stripe, lanes over its slices.
+__global__ __launch_bounds__(256) void k_slice_map(const u32 *sfirst, u32 nstripes, u64 *smap)
 {
     const u32 p = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (p >= nstripes)
         return;
     const u32 a = sfirst[p], n = sfirst[p + 1] - a;
-    const u64 s = order ? order[p] : p;
     for (u32 j = threadIdx.x & 63; j < n; j += 64)
-        smap[a + j] = (s << 32) | j;
+        smap[a + j] = (u64(p) << 32) | j;
 }
 
 // ----------------------------------------------------------------- launchers
@@ -1049,7 +961,7 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
                                  int navail, void *work, int32_t *status, const void *gf, int units, int waves,
                                  int cus, hipStream_t st)
 {
-    if (g->k > 8 || (reinterpret_cast<uintptr_t>(g->parts) & 15) || (reinterpret_cast<uintptr_t>(work) & 3) || (!g->block_sizes && (g->part_pitch & 15)) ||
+    if (g->k > 8 || (reinterpret_cast<uintptr_t>(g->parts) & 15) || (!g->block_sizes && (g->part_pitch & 15)) ||
         (g->block_sizes && g->nstripes > 64u * 1024u))  // k_slice_scan: 64 stripes per thread
         return -ENOSYS;
     if (!g->nstripes)
@@ -1075,8 +987,7 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         smap = reinterpret_cast<u64 *>(reinterpret_cast<u8 *>(scan) + head);
         hipLaunchKernelGGL(k_slice_scan, dim3(1), dim3(1024), 0, st, g->block_sizes, g->order, g->nstripes, g->k,
                            1024u * u32(units), scan, scan + g->nstripes + 1);
-        hipLaunchKernelGGL(k_slice_map, dim3((g->nstripes + 3) / 4), dim3(256), 0, st, scan, g->order, g->nstripes,
-                           smap);
+        hipLaunchKernelGGL(k_slice_map, dim3((g->nstripes + 3) / 4), dim3(256), 0, st, scan, g->nstripes, smap);
     }
     const u32 *stotal = scan ? scan + g->nstripes + 1 : nullptr;
     int rc = 0;

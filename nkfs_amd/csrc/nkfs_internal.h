@@ -104,11 +104,6 @@ int nkfs_launch_synth_ragged(uint8_t *blocks, const uint64_t *block_off, const u
 /* Compute units of the library's device (persistent grids). */
 int nkfs_cu_count(void);
 
-/* Bytes of one stripe's decode plan in the work buffer: K selected slots
- * then the K x K inverse, padded to whole dwords (the slice decoder loads it
- * as dwords). */
-#define NKFS_PLAN_STRIDE(k) ((((uint64_t)(k) + (uint64_t)(k) * (uint64_t)(k)) + 3u) & ~(uint64_t)3u)
-
 /* Sizes shared by host and launchers. */
 uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k);
 size_t nkfs_gf_tables_bytes(void);
