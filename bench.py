@@ -189,6 +189,20 @@ def barrier():
 
 # ----------------------------------------------------------------- timing
 
+def phase(name, fn, check, device):
+    """Run one library call of a step.  With `check` (the first warmup step)
+    the device is synchronised after it, so an asynchronous fault is reported
+    against the call that caused it instead of the next call that happens to
+    read the runtime's sticky error."""
+    import torch
+    try:
+        fn()
+        if check:
+            torch.cuda.synchronize(device)
+    except (OSError, RuntimeError) as ex:
+        raise RuntimeError(f"{name}: {ex}") from ex
+
+
 def timed_steps(step, steps, warmup, device, stream, nev=2):
     """W untimed steps, then exactly `steps` timed steps bracketed by a
     barrier + synchronize on both sides (max over ranks).  Returns
@@ -322,18 +336,20 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
     work = batch.decode_workspace(S, k, device)
     status = torch.empty(S, dtype=torch.int32, device=device)
 
-    def step(e):
+    def step(e, check=False):
         if e:
             e[0].record(stream)
-        batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream)
+        phase(f"{name} encode", lambda: batch.encode(blocks, B, n, k, ids, parts, digests, stream=stream), check,
+              device)
         if e:
             e[1].record(stream)
-        batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status, stream=stream)
+        phase(f"{name} decode", lambda: batch.decode(parts, n, ids, avail, k, B, out=out, work=work, status=status,
+                                                     stream=stream), check, device)
         if e:
             e[2].record(stream)
 
-    for _ in range(args.warmup):
-        step(None)
+    for w in range(args.warmup):
+        step(None, check=w == 0)
     if steps is None:
         steps = auto_steps(step, device, args.steps)
     elapsed, (enc_s, dec_s) = timed_steps(step, steps, 0, device, stream)
@@ -440,18 +456,20 @@ def run_ragged(args, rank, world, device, steps):
     status = torch.empty(S, dtype=torch.int32, device=device)
     maxB = int(gsizes.max())
 
-    def step(e):
+    def step(e, check=False):
         if e:
             e[0].record(stream)
-        batch.encode_ragged(blocks, bo, sz, n, k, ids, parts, po, digests, maxB, stream=stream)
+        phase("c5 encode_ragged", lambda: batch.encode_ragged(blocks, bo, sz, n, k, ids, parts, po, digests, maxB,
+                                                              stream=stream), check, device)
         if e:
             e[1].record(stream)
-        batch.decode_ragged(parts, po, n, ids, avail, k, out, bo, sz, maxB, work=work, status=status, stream=stream)
+        phase("c5 decode_ragged", lambda: batch.decode_ragged(parts, po, n, ids, avail, k, out, bo, sz, maxB,
+                                                              work=work, status=status, stream=stream), check, device)
         if e:
             e[2].record(stream)
 
-    for _ in range(args.warmup):
-        step(None)
+    for w in range(args.warmup):
+        step(None, check=w == 0)
     if steps is None:
         steps = auto_steps(step, device, args.steps)
     elapsed, (enc_s, dec_s) = timed_steps(step, steps, 0, device, stream)
