@@ -622,15 +622,20 @@ out:
 	return rc;
 }
 
-/* Last stage: wait for the context's stream, hand the small outputs to the
- * caller (digests / status / badmask), scatter decoded pages. */
-static int retire(const struct hp *h, struct ctxs *x)
+/* Last stage: wait for the context's stream, then -- only for a sub-batch
+ * whose stages all succeeded (`publish`; a decode's blocks copied back) --
+ * hand the small outputs to the caller (digests / status / badmask) and
+ * scatter decoded pages.  After a failure the staging may hold an earlier
+ * sub-batch's bytes, so nothing of it reaches the caller. */
+static int retire(const struct hp *h, struct ctxs *x, int publish)
 {
 	int rc = 0;
 	const struct sub *u = &x->u;
 	const uint32_t cnt = u->s1 - u->s0;
 	const int nsl = hp_slots(h);
 	HIPGO(hipStreamSynchronize(x->c->stream), "pipeline sync");
+	if (!publish || (h->dir == HP_DEC && !u->copied))
+		goto out;
 	if (h->dir == HP_ENC) {
 		if (h->digests)
 			memcpy(h->digests + (uint64_t)u->s0 * nsl, x->hb + x->L.h_dig, (size_t)cnt * nsl * 8);
@@ -693,7 +698,7 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 	uint32_t it = 0;
 	for (uint32_t s = s0; s < s1 && !rc; it++) {
 		struct ctxs *x = &xs[it % NSTREAM];
-		if (x->u.live && (rc = retire(h, x)))
+		if (x->u.live && (rc = retire(h, x, 1)))
 			break;
 		hipEvent_t ev = x->u.ev;
 		memset(&x->u, 0, sizeof(x->u));
@@ -720,7 +725,7 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 		int r = 0;
 		if (!rc && h->dir == HP_DEC && !x->u.copied)
 			r = copy_blocks(h, x);
-		int r2 = retire(h, x);
+		int r2 = retire(h, x, !rc && !r);
 		if (!rc)
 			rc = r ? r : r2;
 	}
@@ -773,6 +778,8 @@ static int hp_run(struct hp *h)
 		nl = (int)h->nstripes;
 	if (nl <= 1) {
 		rc = run_lane(h, lanes[0], 0, h->nstripes);
+		/* the lane made its device current: hand the library's back */
+		nkfs_use_device(nkfs_gpu_device());
 	} else {
 		struct lane L[NKFS_MAX_DEVICES];
 		pthread_t th[NKFS_MAX_DEVICES];
