@@ -213,69 +213,6 @@ __global__ __launch_bounds__(256) void k_xxh64_batch(const u8 *base, const u64 *
     out[msg] = xxh_tail(h, p + (nst << 5), u32(len & 31));
 }
 
-// Streaming XXH64 for the csum_*/XXH64_* compatibility entry points: fold
-// `nst` whole 32-byte stripes into the four accumulators of one state
-// (crt/xxhash.c:788-821), then (separately) finish.  One message is one
-// serial chain per accumulator, so four lanes do the rounds; the whole wave
-// streams the input: every lane loads 32 B of the next 2 KiB piece
-// (coalesced) while lanes 0-3 fold the current piece from LDS, so no round
-// waits on a global load.
-__global__ __launch_bounds__(64) void k_xxh64_stripes(u64 *state_v, const u8 *data, u64 nst)
-{
-    __shared__ u64 buf[2][64 * 4 + 4];  // piece = 64 stripes; +4: stagger the two halves
-    const int li = threadIdx.x;
-    const int a = li & 3;
-    u64 acc = li < 4 ? state_v[a] : 0;
-    const u64 *src = reinterpret_cast<const u64 *>(data);
-    const u64 pieces = (nst + 63) / 64;
-    u64 w[4] = {0, 0, 0, 0};
-    auto load = [&](u64 p) {
-        const u64 st = p * 64 + u64(li);  // this lane's stripe
-        if (p < pieces && st < nst)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                w[q] = src[st * 4 + q];
-    };
-    load(0);
-    for (u64 p = 0; p < pieces; ++p) {
-        u64 *b = buf[p & 1];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            b[li * 4 + q] = w[q];
-        __syncthreads();
-        load(p + 1);  // in flight under this piece's rounds
-        const u32 cnt = u32(nst - p * 64 < 64 ? nst - p * 64 : 64);
-        if (li < 4) {
-            // 8 rounds per group, their words read together: the serial
-            // chain never waits on an LDS read
-            u32 r = 0;
-            for (; r + 8 <= cnt; r += 8) {
-                u64 wv[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    wv[j] = b[(r + j) * 4 + a];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    acc = xxh_round(acc, wv[j]);
-            }
-            for (; r < cnt; ++r)
-                acc = xxh_round(acc, b[r * 4 + a]);
-        }
-    }
-    if (li < 4)
-        state_v[a] = acc;
-}
-
-__global__ void k_xxh64_finish(u64 *out, const u64 *state_v, u64 total_len, u64 seed, const u8 *tail,
-                               u32 tail_len)
-{
-    if (threadIdx.x != 0)
-        return;
-    u64 h = total_len >= 32 ? xxh_converge(state_v[0], state_v[1], state_v[2], state_v[3]) : seed + XP5;
-    h += total_len;
-    *out = xxh_tail(h, tail, tail_len);
-}
-
 // ------------------------------------------------------------- decode
 //
 // Per stripe: pick the first k offered parts with distinct ids
@@ -815,20 +752,6 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         return rc;
     hipLaunchKernelGGL(k_verify_generic, dim3(g->nstripes), dim3(64), 0, st, *g, n_slots, (const u8 *)work, status,
                        expect, badmask);
-    return launch_ok();
-}
-
-extern "C" int nkfs_launch_xxh64_stripes(uint64_t *state_v, const uint8_t *data, uint64_t nst, void *stream)
-{
-    hipLaunchKernelGGL(k_xxh64_stripes, dim3(1), dim3(64), 0, (hipStream_t)stream, state_v, data, nst);
-    return launch_ok();
-}
-
-extern "C" int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v, uint64_t total_len,
-                                        uint64_t seed, const uint8_t *tail, uint32_t tail_len, void *stream)
-{
-    hipLaunchKernelGGL(k_xxh64_finish, dim3(1), dim3(64), 0, (hipStream_t)stream, out, state_v, total_len, seed,
-                       tail, tail_len);
     return launch_ok();
 }
 

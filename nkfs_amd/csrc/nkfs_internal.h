@@ -52,12 +52,6 @@ int nkfs_launch_decode(const struct nkfs_geom *g, int n_slots,
 		       const uint8_t *ids, const uint8_t *avail, int navail,
 		       void *work, int32_t *status, const void *gf_tables,
 		       void *stream, const uint64_t *expect, uint64_t *badmask);
-int nkfs_launch_xxh64_stripes(uint64_t *state_v, const uint8_t *data,
-			      uint64_t nstripes32, void *stream);
-int nkfs_launch_xxh64_finish(uint64_t *out, const uint64_t *state_v,
-			     uint64_t total_len, uint64_t seed,
-			     const uint8_t *tail, uint32_t tail_len,
-			     void *stream);
 /* One message's XXH64 chains in one wave (xxh64_chain.hip): fold `nst`
  * 32-byte stripes at `src` (a device-visible pointer: pinned host memory or
  * device memory) into the accumulators -- from v[] or, with FROM_DEV, from
