@@ -363,6 +363,32 @@ def test_host_register_api(L):
     assert L.nkfs_host_register(pinned.data_ptr(), 4096) == -17  # -EEXIST: runtime-pinned
 
 
+def test_partial_overlap_with_registration_is_busy(L):
+    """A host call whose buffer starts inside a range this library pinned
+    (nkfs_host_register) but runs past its end is refused with -EBUSY before
+    any copy, instead of DMA-ing from memory the owner may unpin mid-copy
+    (pipeline.c pin_take); the range alone and the range inside
+    the registration both work."""
+    from nkfs_amd import batch
+    B, n, k = 65536, 8, 5
+    buf = np.zeros(4 * B, np.uint8)
+    buf[:] = np.frombuffer(np.random.default_rng(5).bytes(buf.nbytes), np.uint8)
+    ids_np = synth.batch_ids(2, n, first=77)
+    assert L.nkfs_host_register(buf.ctypes.data, 2 * B) == 0
+    try:
+        inside = buf[: 2 * B].reshape(2, B)
+        p_in, d_in = batch.encode_host(inside, B, n, k, ids_np)
+        straddle = buf[B: 3 * B].reshape(2, B)
+        with pytest.raises(OSError) as ei:
+            batch.encode_host(straddle, B, n, k, ids_np)
+        assert ei.value.errno == 16  # EBUSY
+    finally:
+        assert L.nkfs_host_unregister(buf.ctypes.data) == 0
+    p_out, d_out = batch.encode_host(buf[B: 3 * B].reshape(2, B), B, n, k, ids_np)  # unregistered: fine
+    p_ref, d_ref = batch.encode_host(np.ascontiguousarray(buf[B: 3 * B]).reshape(2, B), B, n, k, ids_np)
+    assert torch.equal(d_out, d_ref)
+
+
 # ---------------------------------------------------------------- general path, big parts
 
 def test_generic_parts_beyond_grid_y(L, O):
