@@ -53,11 +53,11 @@ CONFIGS = {
                                 "per GPU"),
     "c4": (16384, 262144, 8, 5, "C4: N=8,K=5 encode(+XXH64/part)+decode(3 erased), 16384 x 256 KiB stripes per GPU"),
     # beyond the BASELINE configs: n > 8, k > 8 (SURVEY.md §8 a5/a8 for general n, k) on the
-    # part-group encoder and survivor-table decoder (nk8_wide.hip); XXH64 is a second pass over the parts
+    # part-group encoder with XXH64 fused (k_encode_wide_ws) and the survivor-table decoder (nk8_wide.hip)
     "w1": (2048, 1048576, 16, 12, "W1: N=16,K=12 encode(+XXH64/part)+decode(4 erased), 2048 x 1 MiB stripes per "
                                   "GPU (general n,k path; not a BASELINE config)"),
     # k > 16 (the reference allows k <= 254, crt/nk8.c:13-16; its self test draws k uniform in [2, 254],
-    # crt/nk8.c:735-744): the general-k kernels
+    # crt/nk8.c:735-744): the column-chunked kernels (nk8_big.hip), XXH64 a second pass over the parts
     "w2": (256, 1048576, 48, 32, "W2: N=48,K=32 encode(+XXH64/part)+decode(16 erased), 256 x 1 MiB stripes per "
                                  "GPU (k > 16 path; not a BASELINE config)"),
     # ragged: block size of every stripe drawn from C5_SIZES (synth.mixed_sizes)
