@@ -209,7 +209,12 @@ int nkfs_pages_dsum_batch(const uint8_t *const *d_pages,
  * part bytes between a part's size and its pitch are unspecified, bytes
  * between stripes and the blocks of stripes that fail to decode
  * (-EINVAL: fewer than k distinct ids) keep the caller's contents.
- * The calling thread is left with the library's device current. */
+ * A buffer that starts inside a range registered through
+ * nkfs_host_register but runs past its end is refused with -EBUSY (its
+ * owner could unpin the registered part mid-copy); a call that fails
+ * publishes no status, digests or decoded pages of the sub-batches it did
+ * not finish.  The calling thread is left with the library's device
+ * current. */
 
 /* Pin a host range for the library's DMA once (e.g. a server's page pool),
  * so per-call pinning becomes a reference bump.  -EEXIST when the runtime
