@@ -66,8 +66,10 @@ int nkfs_gpu_get_devices(int *devices, int max);
 enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG,
        NKFS_ENC_WIDE_WS };
 /* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16);
- * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16) */
-enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG };
+ * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16);
+ * NKFS_DEC_RUN: run decoder (k <= 8: persistent waves, each walking one
+ * contiguous run of 1,024-row units across stripes) */
+enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG, NKFS_DEC_RUN };
 struct nkfs_tune {
 	int enc_kernel;       /* NKFS_ENC_*: encoder (WIDE / GENERIC also pin n <= 8 shapes) */
 	int dec_kernel;       /* NKFS_DEC_*: decoder (WIDE / GENERIC also pin k <= 8) */

@@ -35,7 +35,7 @@ class Tune(C.Structure):
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4, "wide": 5, "big": 6, "wide_ws": 7}
-DEC = {"auto": 0, "slice": 1, "wave": 2, "generic": 3, "wide": 4, "big": 5}
+DEC = {"auto": 0, "slice": 1, "wave": 2, "generic": 3, "wide": 4, "big": 5, "run": 6}
 
 # name -> (restype, argtypes)
 _SIGS = {

@@ -184,6 +184,18 @@ __device__ inline u64 shfl64(u64 v, int src)
     return (u64(hi) << 32) | lo;
 }
 
+// Run decoder workspace layout (nk8_walk.hip, k_run_plan / k_decode_run)
+__host__ __device__ inline u32 run_plan_stride(int k) { return (u32(k + k * k) + 3u) & ~3u; }
+__host__ __device__ inline u64 run_loc_off(u32 nstripes, int k)
+{
+    return (u64(nstripes) * run_plan_stride(k) + 15u) & ~u64(15);
+}
+__host__ __device__ inline u64 run_gsum_off(u32 nstripes, int k)
+{
+    return (run_loc_off(nstripes, k) + u64(nstripes) * 4u + 15u) & ~u64(15);
+}
+
+
 struct Stripe {
     const u8 *blk;
     u8 *parts;

@@ -544,9 +544,14 @@ static u32 max_part_size(const nkfs_geom *g, u32 max_block)
 
 extern "C" size_t nkfs_gf_tables_bytes(void) { return sizeof(GfTables); }
 
+extern "C" uint64_t nkfs_run_work_bytes(uint32_t nstripes, int k);
+
+// the larger of the plan layouts: k + k*k bytes per stripe (k_decode_plan,
+// k_decode_prep) and the run decoder's padded plans + unit prefixes
 extern "C" uint64_t nkfs_decode_work_bytes(uint32_t nstripes, int k)
 {
-    return u64(nstripes) * u64(k + k * k);
+    const u64 a = u64(nstripes) * u64(k + k * k), b = nkfs_run_work_bytes(nstripes, k);
+    return a > b ? a : b;
 }
 
 extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
@@ -588,6 +593,9 @@ extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const i
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                  void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                  hipStream_t st);
+extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
+                               void *work, int32_t *status, const void *gf, int units, int waves, int cus,
+                               hipStream_t st);
 
 // Fast-path encoder choice (n <= 8, k <= 8), struct nkfs_tune.enc_kernel:
 // AUTO = the walk encoder for ragged batches (one wave per stripe in size
@@ -710,6 +718,9 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // k = 2 a 4 KiB stripe is one wave either way and the wave decoder's
         // in-wave inverse saves the plan launch
         const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel : g->k >= 3 ? NKFS_DEC_SLICE : NKFS_DEC_WAVE;
+        if (kern == NKFS_DEC_RUN && !expect)
+            rc = nkfs_run_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_units, t.dec_waves_per_cu,
+                                 nkfs_cu_count(), st);
         if (kern == NKFS_DEC_SLICE && !expect) {
             // ragged: in size order (largest first), so the grid's tail is short slices
             auto slice = [&](const nkfs_geom *go) {

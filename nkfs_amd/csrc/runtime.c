@@ -73,7 +73,7 @@ void nkfs_tune_get(struct nkfs_tune *t)
 int nkfs_tune_set(const struct nkfs_tune *t)
 {
 	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WIDE_WS || t->dec_kernel < NKFS_DEC_AUTO ||
-	    t->dec_kernel > NKFS_DEC_BIG || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
+	    t->dec_kernel > NKFS_DEC_RUN || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||

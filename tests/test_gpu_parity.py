@@ -609,7 +609,7 @@ def test_slice_decode_matches(L, O, n, k, B, S):
         ids_np2[1, av[1, 1]] = ids_np2[1, av[1, 0]]
         ids_np2[2, :] = ids_np2[2, 0]
     outs = []
-    for kern, units in (("wave", 2), ("slice", 1), ("slice", 2), ("slice", 4)):
+    for kern, units in (("wave", 2), ("slice", 1), ("slice", 2), ("slice", 4), ("run", 1), ("run", 2), ("run", 4)):
         with _tuned(dec_kernel=_dec(kern), dec_units=units):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             o, st = batch.decode(parts, n, dev(ids_np2), dev(np.ascontiguousarray(av)), k, B, out=out)
@@ -769,7 +769,8 @@ def test_ragged_slice_decode_matches_wave(L, n, k, units):
     ids2 = ids_np.copy()
     ids2[3, :] = ids2[3, 0]  # stripe 3: one distinct id
     outs = []
-    for kern, pp, po in (("wave", parts, poff), ("slice", parts, poff), ("slice", parts2, poff2)):
+    for kern, pp, po in (("wave", parts, poff), ("slice", parts, poff), ("slice", parts2, poff2), ("run", parts, poff),
+                         ("run", parts2, poff2)):
         with _tuned(dec_kernel=_dec(kern), dec_units=units):
             out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
             st = batch.decode_ragged(pp, dev(po), n, dev(ids2), dev(avail), k, out, dev(boff),
@@ -809,7 +810,7 @@ def test_ragged_slice_decode_past_2gib(L, n, k, units):
     batch.encode_ragged(blocks, dev(boff), sz, n, k, dev(ids_np), parts, dev(poff), None, int(sizes.max()))
     avail = synth.batch_survivors(len(sizes), n, k, first=900)
     res = []
-    for kern in ("slice", "wave"):
+    for kern in ("slice", "wave", "run"):
         with _tuned(dec_kernel=_dec(kern), dec_units=units):
             out = torch.zeros(pos, dtype=torch.uint8, device="cuda")
             st = batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(avail), k, out, dev(boff), sz,
@@ -818,7 +819,7 @@ def test_ragged_slice_decode_past_2gib(L, n, k, units):
             assert int(st.abs().sum()) == 0
             res.append(out[base:].cpu())
             del out
-    assert torch.equal(res[0], res[1])
+    assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])
     assert np.array_equal(res[0].numpy(), host)
     del parts, blocks
     torch.cuda.empty_cache()
@@ -849,8 +850,64 @@ def test_bench_kernels_against_oracle(L, O, S, B):
             assert np.array_equal(parts[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), (kern, s)
             assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], (kern, s)
     avail = dev(synth.batch_survivors(S, n, k, first=4242))
-    with _tuned(dec_kernel=_dec("slice")):
-        out, status = batch.decode(parts, n, ids, avail, k, B)
+    for kern in ("slice", "run"):
+        with _tuned(dec_kernel=_dec(kern)):
+            out, status = batch.decode(parts, n, ids, avail, k, B)
+        torch.cuda.synchronize()
+        assert int(status.abs().sum()) == 0
+        assert torch.equal(out, blocks[:, :B]), kern
+
+
+@pytest.mark.parametrize("n,k,waves,units", [(8, 5, 12, 2), (4, 2, 12, 2), (6, 3, 1, 4), (8, 8, 32, 1),
+                                             (5, 4, 2, 4), (3, 2, 32, 2)])
+def test_run_decode_walks_across_stripes(L, O, n, k, waves, units):
+    """The run decoder (nk8_walk.hip k_run_plan + k_decode_run): every
+    resident wave walks one contiguous run of 1,024-row units across stripe
+    boundaries, with the next stripe's descriptor loaded ahead.  Runs that
+    start and end inside stripes, stripes with too few distinct ids
+    (-EINVAL, skipped, block untouched) at run boundaries and in a row,
+    one-byte / k+1-byte / unit-boundary sizes, more waves than units
+    (waves = 32 on a small batch) and a few long runs (waves = 1): blocks
+    equal to the oracle's input, statuses equal to the wave decoder's
+    (crt/nk8.c:446-599)."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(300, (4096, 65536, 1048576, 1, k + 1, 1024 * k, 1024 * k + 1, 3 * 1024 * k - 1))
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, 3)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(7000 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=7000)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff),
+                        None, int(sizes.max()))
+    avail = synth.batch_survivors(len(sizes), n, k, first=7000)
+    ids2 = ids_np.copy()
+    bad = {0, 17, 18, 19, 150, len(sizes) - 1}
+    for s in bad:
+        ids2[s, :] = ids2[s, 0]
+    outs = []
+    for kern in ("wave", "run"):
+        with _tuned(dec_kernel=_dec(kern), dec_units=units, dec_waves_per_cu=waves):
+            out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+            st = batch.decode_ragged(parts, dev(poff), n, dev(ids2), dev(avail), k, out, dev(boff),
+                                     dev(sizes.astype(np.int32)), int(sizes.max()))
+            torch.cuda.synchronize()
+            outs.append((out.cpu(), st.cpu().tolist()))
+    assert outs[1][1] == outs[0][1]
+    assert torch.equal(outs[1][0], outs[0][0])
+    o, st = outs[1]
+    for s, B in enumerate(sizes):
+        if s in bad:
+            assert st[s] == -22 and bool((o[boff[s]: boff[s] + B] == 0xEE).all()), s
+        else:
+            assert st[s] == 0 and np.array_equal(o[boff[s]: boff[s] + B].numpy(), host[boff[s]: boff[s] + B]), s
+    # uniform: C2's shape (two units per stripe) through the same walk
+    S, B = 3000, 4096
+    blocks = batch.synth(S, B, first=77)
+    uid = synth.batch_ids(S, n, first=77)
+    up, _ = batch.encode(blocks, B, n, k, dev(uid))
+    uav = dev(synth.batch_survivors(S, n, k, first=77))
+    with _tuned(dec_kernel=_dec("run"), dec_units=units, dec_waves_per_cu=waves):
+        out, status = batch.decode(up, n, dev(uid), uav, k, B)
     torch.cuda.synchronize()
-    assert int(status.abs().sum()) == 0
-    assert torch.equal(out, blocks[:, :B])
+    assert int(status.abs().sum()) == 0 and torch.equal(out, blocks[:, :B])
