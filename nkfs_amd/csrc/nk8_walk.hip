@@ -836,415 +836,6 @@ __global__ __launch_bounds__(256) void k_slice_map(const u32 *sfirst, u32 nstrip
         smap[a + j] = (u64(p) << 32) | j;
 }
 
-// ------------------------------------------------------------ run decoder
-//
-// k_run_plan<K> + k_decode_run<K,E,U,RAGGED>: the batch's 1,024-row units
-// (stripe by stripe, batch order) are cut into one contiguous run per
-// resident wave, equal in units.  A wave finds its first (stripe, unit) once
-// and then walks: a stripe's tables are built when the wave enters it, and
-// the next stripe's descriptor (size, offsets, selection and inverse) is
-// loaded when it enters the current one, so no unit waits on a metadata
-// chain.  The plan kernel also leaves every stripe's unit count prefix
-// (within its 256-stripe group) and each group's total in the caller's
-// workspace: no scratch allocation, no single-workgroup setup launch.
-//
-// Workspace (nkfs_decode_work_bytes): plan[s] at s * run_plan_stride(k)
-// (k slots, then W row-major; slot byte 0xFF: fewer than k distinct ids),
-// then u32 loc[nstripes] (exclusive prefix of the units of the stripes
-// before s in its group), then u32 gsum[ceil(nstripes / 256)].
-// units of 1,024 rows of a stripe (0: nothing to rebuild)
-__device__ inline u32 run_units(u32 B, int k) { return (part_size_of(B, k) + 1023u) >> 10; }
-
-template <int K>
-__global__ __launch_bounds__(256) void k_run_plan(const nkfs_geom g, const u8 *ids, const u8 *avail, int n_slots,
-                                                  int navail, u8 *work, int32_t *status, const GfTables *gft)
-{
-    constexpr u32 PS = (K + K * K + 3) & ~3;
-    __shared__ u32 wtot[4];
-    const u32 s = blockIdx.x * 256u + threadIdx.x;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    u32 units = 0;
-    if (s < g.nstripes) {
-        const u8 *sid = ids + u64(s) * n_slots;
-        const u8 *sav = avail + u64(s) * navail;
-        u8 *pl = work + u64(s) * PS;
-        u32 x[K], sl[K];
-        int h = 0;
-        for (int c = 0; c < navail && h < K; ++c) {  // crt/nk8.c:512-537
-            const u32 slot = sav[c];
-            const u32 id = sid[slot];
-            bool dup = false;
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                dup |= j < h && x[j] == id;
-            if (dup)
-                continue;
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                if (j == h) {
-                    x[j] = id;
-                    sl[j] = slot;
-                }
-            ++h;
-        }
-        if (status)
-            status[s] = h < K ? -EINVAL : 0;
-        if (h < K) {
-            pl[0] = 0xFF;
-        } else {
-            units = run_units(g.block_sizes ? g.block_sizes[s] : g.block_size, K);
-            // W = V^-1 in closed form, as k_decode_plan (crt/nk8.c:199-266)
-            u32 M[K + 1];
-            M[0] = 1;
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                M[c + 1] = M[c];
-#pragma unroll
-                for (int i = c; i >= 1; --i)
-                    M[i] = M[i - 1] ^ gfm_bits(x[c], M[i]);
-                M[0] = gfm_bits(x[c], M[0]);
-            }
-            u32 words[PS / 4];
-#pragma unroll
-            for (int i = 0; i < int(PS / 4); ++i)
-                words[i] = 0;
-            auto put = [&](int at, u32 v) {
-#pragma unroll
-                for (int i = 0; i < int(PS / 4); ++i)
-                    if (i == at / 4)
-                        words[i] |= (v & 0xFFu) << (8 * (at % 4));
-            };
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                put(c, sl[c]);
-                u32 q[K];
-                u32 a = M[K];
-                q[K - 1] = a;
-#pragma unroll
-                for (int i = K - 1; i >= 1; --i) {
-                    a = M[i] ^ gfm_bits(x[c], a);
-                    q[i - 1] = a;
-                }
-                u32 dd = 0;
-#pragma unroll
-                for (int i = K - 1; i >= 0; --i)
-                    dd = gfm_bits(dd, x[c]) ^ q[i];
-                const u32 dinv = gft->inv[dd];
-#pragma unroll
-                for (int i = 0; i < K; ++i)
-                    put(K + c * K + i, gfm_bits(q[i], dinv));
-            }
-#pragma unroll
-            for (int i = 0; i < int(PS / 4); ++i)
-                reinterpret_cast<u32 *>(pl)[i] = words[i];
-        }
-    }
-    // exclusive prefix of the units within the 256-stripe group
-    u32 inc = units;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 y = __shfl_up(inc, d, 64);
-        if (lane >= d)
-            inc += y;
-    }
-    if (lane == 63)
-        wtot[wv] = inc;
-    __syncthreads();
-    u32 before = 0;
-    for (int i = 0; i < wv; ++i)
-        before += wtot[i];
-    u32 *loc = reinterpret_cast<u32 *>(work + run_loc_off(g.nstripes, K));
-    if (s < g.nstripes)
-        loc[s] = before + inc - units;
-    if (threadIdx.x == 255)
-        reinterpret_cast<u32 *>(work + run_gsum_off(g.nstripes, K))[blockIdx.x] = before + inc;
-}
-
-// A stripe's descriptor as the walk needs it: plan words, part size, part
-// pitch, part base and block base (all wave-uniform, held in VGPRs and
-// loaded by vector loads: a scalar load shares lgkmcnt with the LDS traffic,
-// so waiting on any LDS access would wait on the prefetch too).
-template <int K, bool RAGGED>
-struct RunDesc {
-    static constexpr int PW = (K + K * K + 3) / 4;
-    u32 pw[PW];
-    u32 B;
-    u64 poff;
-    u64 boff;
-};
-
-template <int K, bool RAGGED>
-__device__ inline void run_desc_load(const nkfs_geom &g, int n_slots, const u8 *work, u32 s, u32 vz,
-                                     RunDesc<K, RAGGED> &d)
-{
-    // vz: 0 at run time, but a VGPR -- keeps these loads on the vector path
-    const u32 *pw = reinterpret_cast<const u32 *>(work + u64(s) * run_plan_stride(K)) + vz;
-#pragma unroll
-    for (int i = 0; i < RunDesc<K, RAGGED>::PW; ++i)
-        d.pw[i] = pw[i];
-    if constexpr (RAGGED) {
-        d.B = g.block_sizes[s + vz];
-        d.poff = g.part_off[s + vz];
-        d.boff = g.block_off[s + vz];
-    } else {
-        d.B = g.block_size;
-        d.poff = u64(s) * u64(n_slots) * g.part_pitch;
-        d.boff = u64(s) * g.block_pitch;
-    }
-}
-
-template <int K, int E, int U, bool RAGGED>
-__global__ __launch_bounds__(64) void k_decode_run(nkfs_geom g, int n_slots, const u8 *work)
-{
-    constexpr int W = E / 4;
-    constexpr int TB = 256 * E;
-    constexpr int LS = 16 * K + (K % 2 == 0 ? 16 : 0);  // transpose bytes per lane (even K padded)
-    constexpr bool XPOSE = K >= 3;
-    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
-    __shared__ __attribute__((aligned(16))) u8 obuf[XPOSE ? 64 * LS : 16];
-    const int li = threadIdx.x;
-    u32 vz;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-
-    // ---- this wave's run: units [u0, u1) of the batch's T units
-    const u32 ngroups = (g.nstripes + 255u) / 256u;
-    const u32 *gsum = reinterpret_cast<const u32 *>(work + run_gsum_off(g.nstripes, K));
-    const u32 *loc = reinterpret_cast<const u32 *>(work + run_loc_off(g.nstripes, K));
-    u64 T = 0;
-    for (u32 c = 0; c < ngroups; c += 64) {
-        const u32 i = c + u32(li);
-        u64 v = i < ngroups ? gsum[i] : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1)
-            v += __shfl_xor(v, d, 64);
-        T += v;
-    }
-    const u64 u0 = T * blockIdx.x / gridDim.x, u1 = T * (blockIdx.x + 1u) / gridDim.x;
-    if (u0 >= u1)
-        return;
-    // group holding unit u0: the first whose inclusive prefix exceeds u0
-    u64 base = 0;
-    u32 grp = 0;
-    for (u32 c = 0;; c += 64) {  // u0 < T: some group is found
-        const u32 i = c + u32(li);
-        const u64 v = i < ngroups ? gsum[i] : 0u;
-        u64 inc = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u64 y = __shfl_up(inc, d, 64);
-            if (li >= d)
-                inc += y;
-        }
-        const u64 hit = __ballot(base + inc > u0);
-        if (hit) {
-            const int f = __builtin_ctzll(hit);
-            grp = c + u32(f);
-            base += __shfl(inc - v, f, 64);
-            break;
-        }
-        base += __shfl(inc, 63, 64);
-    }
-    // stripe holding u0: the last of the group whose prefix is <= u0 (the
-    // prefix is monotone, so a count of the lanes that pass)
-    u32 s = grp * 256u;
-    {
-        int cnt = 0;
-        u32 lq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const u32 i = grp * 256u + u32(64 * q + li);
-            lq[q] = i < g.nstripes ? loc[i] : 0xFFFFFFFFu;
-            cnt += __popcll(__ballot(i < g.nstripes && base + lq[q] <= u0));
-        }
-        const int sl = cnt - 1;  // >= 0: loc of the group's first stripe is 0
-        u32 ls = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const u32 y = __shfl(lq[q], sl & 63, 64);
-            if (q == (sl >> 6))
-                ls = y;
-        }
-        s += u32(sl);
-        base += ls;  // first unit of stripe s
-    }
-    u32 u = u32(u0 - base);  // unit within stripe s
-    u64 left = u1 - u0;
-
-    RunDesc<K, RAGGED> cur, nxt;
-    run_desc_load<K, RAGGED>(g, n_slots, work, s, vz, cur);
-    if (s + 1 < g.nstripes)
-        run_desc_load<K, RAGGED>(g, n_slots, work, s + 1, vz, nxt);
-    bool fresh = true;  // tables of `cur` not built yet
-    for (;;) {
-        const u32 ps = part_size_of(cur.B, K);
-        const u32 nu = (cur.pw[0] & 0xFFu) == 0xFFu ? 0u : (ps + 1023u) >> 10;
-        if (u >= nu) {  // stripe done (or nothing to rebuild): the next one
-            if (!left || s + 1 >= g.nstripes)
-                return;
-            ++s;
-            cur = nxt;
-            if (s + 1 < g.nstripes)
-                run_desc_load<K, RAGGED>(g, n_slots, work, s + 1, vz, nxt);
-            u = 0;
-            fresh = true;
-            continue;
-        }
-        const u64 ppitch = RAGGED ? (u64(ps) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1) : g.part_pitch;
-        const u8 *pbase = g.parts + cur.poff;
-        u8 *out = const_cast<u8 *>(g.blocks) + cur.boff;
-        const u32 B = cur.B;
-        const bool pal = !RAGGED || (reinterpret_cast<uintptr_t>(pbase) & 15) == 0;
-        const u32 take = min(u32(U), min(nu - u, u32(left < u64(U) ? left : u64(U))));
-        const u32 rbase = u * 1024u;
-
-        // this chunk's loads first (their latency hides under a table build)
-        const u8 *src[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            src[c] = pbase + u64((cur.pw[c / 4] >> (8 * (c % 4))) & 0xFFu) * ppitch;
-        u32 pv[U][K][4];
-#pragma unroll
-        for (int uu = 0; uu < U; ++uu) {
-            const u32 r0 = rbase + uu * 1024 + 16 * li;
-            if (u32(uu) < take && r0 < ps)
-#pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    if (pal) {
-                        const uint4 t = *reinterpret_cast<const uint4 *>(src[c] + r0);  // pitch >= round16(ps)
-                        pv[uu][c][0] = t.x;
-                        pv[uu][c][1] = t.y;
-                        pv[uu][c][2] = t.z;
-                        pv[uu][c][3] = t.w;
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            u32 x = 0;
-                            for (int e = 0; e < 4; ++e)
-                                x |= u32(src[c][r0 + 4 * q + e]) << (8 * e);  // within the pitch
-                            pv[uu][c][q] = x;
-                        }
-                    }
-                }
-        }
-        if (fresh) {
-            __syncthreads();  // the previous stripe's lookups are done
-            // U_c[x] = (W[c][0] x, ..., W[c][K-1] x), packed
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                u32 rw[W];
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    u32 x = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (4 * w + b < K) {
-                            const int at = K + c * K + 4 * w + b;
-                            x |= ((cur.pw[at / 4] >> (8 * (at % 4))) & 0xFFu) << (8 * b);
-                        }
-                    rw[w] = x;
-                }
-                u32 basis[8][W];
-                make_basis<W>(basis, rw);
-                build_table<W, 64>(tbl + c * TB, basis, li);
-            }
-            __syncthreads();
-            fresh = false;
-        }
-
-        const bool aligned = ((reinterpret_cast<uintptr_t>(out) | (RAGGED ? 0 : g.block_pitch)) & 15) == 0;
-#pragma unroll
-        for (int uu = 0; uu < U; ++uu) {
-            if (u32(uu) >= take)
-                break;
-            const u32 ru = rbase + uu * 1024;
-            const u32 r0 = ru + 16 * li;
-            u32 o[4 * K];
-            if (r0 < ps) {
-                u32 ent[2][4][K][W];
-                auto look = [&](int gq, u32 (&e)[4][K][W]) {
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int r = 4 * gq + rr;
-#pragma unroll
-                        for (int c = 0; c < K; ++c) {
-                            const u32 byte = (pv[uu][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                            const u8 *ep = tbl + c * TB + byte * E;
-                            if constexpr (E == 8) {
-                                const uint2 t = *reinterpret_cast<const uint2 *>(ep);
-                                e[rr][c][0] = t.x;
-                                e[rr][c][W - 1] = t.y;
-                            } else {
-                                e[rr][c][0] = *reinterpret_cast<const u32 *>(ep);
-                            }
-                        }
-                    }
-                };
-                look(0, ent[0]);
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    if (gq < 3)
-                        look(gq + 1, ent[(gq + 1) & 1]);
-                    u32 row[4 * W];
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-                        for (int w = 0; w < W; ++w) {
-                            u32 x = ent[gq & 1][rr][0][w];
-#pragma unroll
-                            for (int c = 1; c < K; ++c)
-                                x ^= ent[gq & 1][rr][c][w];
-                            row[rr * W + w] = x;
-                        }
-#pragma unroll
-                    for (int q = 0; q < K; ++q)
-                        o[gq * K + q] = pack_dword<K, W>(row, q);
-                }
-            }
-            const u64 ubyte = u64(ru) * K;  // first output byte of the unit
-            if constexpr (XPOSE) {
-                if (r0 < ps)
-#pragma unroll
-                    for (int q = 0; q < K; ++q)
-                        *reinterpret_cast<uint4 *>(obuf + li * LS + 16 * q) =
-                            make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const int j = q * 64 + li;  // 16-byte piece of the unit's output
-                    const uint4 t = *reinterpret_cast<const uint4 *>(obuf + (j / K) * LS + (j % K) * 16);
-                    const u64 off = ubyte + u64(j) * 16;
-                    if (aligned && off + 16 <= B) {
-                        store16(out + off, t.x, t.y, t.z, t.w, false);
-                    } else if (off < B) {
-                        const u32 tw[4] = {t.x, t.y, t.z, t.w};
-                        for (int b = 0; b < 16 && off + b < B; ++b)
-                            out[off + b] = u8(tw[b >> 2] >> (8 * (b & 3)));
-                    }
-                }
-                __syncthreads();
-            } else if (r0 < ps) {
-                const u64 off = u64(r0) * K;
-                if (aligned && off + 16 * K <= B) {
-                    uint4 *dst = reinterpret_cast<uint4 *>(out + off);
-#pragma unroll
-                    for (int q = 0; q < K; ++q)
-                        store16(dst + q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], false);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4 * K; ++q)
-                        for (int b = 0; b < 4; ++b)
-                            if (off + 4 * q + b < B)
-                                out[off + 4 * q + b] = u8(o[q] >> (8 * b));
-                }
-            }
-        }
-        u += take;
-        left -= take;
-        if (!left)
-            return;
-    }
-}
-
 // ----------------------------------------------------------------- launchers
 
 template <int K, int E, int U, int P, bool HASH, bool NIB>
@@ -1422,76 +1013,5 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         rc = -EIO;
     if (rc)
         return rc;
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
-}
-
-// ------------------------------------------------------- run decoder launch
-
-template <int K, int E, int U>
-static void launch_run(hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *work, int waves, int cus)
-{
-    if (g.block_sizes) {
-        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_run<K, E, U, true>), waves);
-        hipLaunchKernelGGL((k_decode_run<K, E, U, true>), dim3(u32(cus) * u32(sh.per_cu)), dim3(64), sh.pad, st, g,
-                           n_slots, work);
-    } else {
-        const Shape sh = occupancy_shape(reinterpret_cast<const void *>(&k_decode_run<K, E, U, false>), waves);
-        hipLaunchKernelGGL((k_decode_run<K, E, U, false>), dim3(u32(cus) * u32(sh.per_cu)), dim3(64), sh.pad, st, g,
-                           n_slots, work);
-    }
-}
-
-template <int K, int E>
-static void launch_run_u(int units, hipStream_t st, const nkfs_geom &g, int n_slots, const u8 *work, int waves,
-                         int cus)
-{
-    if (units >= 4)
-        launch_run<K, E, 4>(st, g, n_slots, work, waves, cus);
-    else if (units == 2)
-        launch_run<K, E, 2>(st, g, n_slots, work, waves, cus);
-    else
-        launch_run<K, E, 1>(st, g, n_slots, work, waves, cus);
-}
-
-extern "C" uint64_t nkfs_run_work_bytes(uint32_t nstripes, int k)
-{
-    return run_gsum_off(nstripes, k) + u64((nstripes + 255u) / 256u) * 4u;
-}
-
-// Run decoder, k <= 8, uniform or ragged (g->order ignored: batch order):
-// k_run_plan (selection, inverse, unit prefix per 256 stripes, in `work`)
-// then one persistent wave per resident slot walking its run of units.
-// -ENOSYS outside its shapes.
-extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                               int navail, void *work, int32_t *status, const void *gf, int units, int waves,
-                               int cus, hipStream_t st)
-{
-    if (g->k > 8 || g->k < 2 || (reinterpret_cast<uintptr_t>(g->parts) & 15) ||
-        (!g->block_sizes && (g->part_pitch & 15)) || (reinterpret_cast<uintptr_t>(work) & 15))
-        return -ENOSYS;
-    if (!g->nstripes)
-        return 0;
-    u8 *w = static_cast<u8 *>(work);
-    const GfTables *gft = static_cast<const GfTables *>(gf);
-    const dim3 pgrid((g->nstripes + 255) / 256);
-    units = units >= 4 ? 4 : units >= 2 ? 2 : 1;
-    switch (g->k) {
-#define NKFS_RK(KK, EE)                                                                                          \
-    case KK:                                                                                                     \
-        hipLaunchKernelGGL((k_run_plan<KK>), pgrid, dim3(256), 0, st, *g, ids, avail, n_slots, navail, w, status, \
-                           gft);                                                                                 \
-        launch_run_u<KK, EE>(units, st, *g, n_slots, w, waves, cus);                                             \
-        break;
-        NKFS_RK(2, 4)
-        NKFS_RK(3, 4)
-        NKFS_RK(4, 4)
-        NKFS_RK(5, 8)
-        NKFS_RK(6, 8)
-        NKFS_RK(7, 8)
-        NKFS_RK(8, 8)
-#undef NKFS_RK
-    default:
-        return -ENOSYS;
-    }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
