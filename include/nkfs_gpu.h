@@ -75,14 +75,14 @@ struct nkfs_tune {
 	int dec_kernel;       /* NKFS_DEC_*: decoder (WIDE / GENERIC also pin k <= 8) */
 	int enc_waves_per_cu; /* resident waves per CU of the walk encoder (1..32) */
 	int dec_waves_per_cu; /* resident waves per CU of the slice decoder (1..32) */
-	int dec_units;        /* 1,024-row units per slice-decoder wave (1, 2 or 4; 8 and 16
-				 run decoder chunks only, the slice decoder takes 4) */
+	int dec_units;        /* 1,024-row units per slice-decoder wave (1, 2 or 4) */
 	int enc_nib;          /* walk encoder, n > 4: nibble product tables (-1 auto, 0, 1) */
 	int enc_units;        /* walk encoder: 1,024-row units per chunk (0 auto, 1, 2; n <= 4 only) */
 	int size_order;       /* ragged batches run largest stripe first (0/1) */
 	int enc_prefetch;     /* walk encoder: chunks of loads in flight ahead of the one encoded (1, 2) */
 	int enc_fused_waves_per_cu; /* fused encoder: resident waves per CU cap (0 = none, 3..32) */
 	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
+	int dec_run_units;    /* run decoder: 1,024-row units per chunk (1, 2, 4, 8, 16) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

@@ -31,7 +31,7 @@ class Tune(C.Structure):
     """struct nkfs_tune (include/nkfs_gpu.h): kernel choice and launch shape."""
     _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
                                        "dec_units", "enc_nib", "enc_units", "size_order", "enc_prefetch",
-                                       "enc_fused_waves_per_cu", "dec_wave_waves_per_cu")]
+                                       "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units")]
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4, "wide": 5, "big": 6, "wide_ws": 7}

@@ -724,7 +724,7 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
                          : g->block_sizes              ? NKFS_DEC_RUN
                                                        : NKFS_DEC_SLICE;
         if (kern == NKFS_DEC_RUN && !expect)
-            rc = nkfs_run_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_units, t.dec_waves_per_cu,
+            rc = nkfs_run_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_run_units, t.dec_waves_per_cu,
                                  nkfs_cu_count(), st);
         if (kern == NKFS_DEC_SLICE && !expect) {
             // ragged: in size order (largest first), so the grid's tail is short slices

@@ -59,6 +59,7 @@ static struct nkfs_tune g_tune = {
 	.enc_prefetch = 1,
 	.enc_fused_waves_per_cu = 0,
 	.dec_wave_waves_per_cu = 0,
+	.dec_run_units = 4,
 };
 
 void nkfs_tune_get(struct nkfs_tune *t)
@@ -75,11 +76,13 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WIDE_WS || t->dec_kernel < NKFS_DEC_AUTO ||
 	    t->dec_kernel > NKFS_DEC_RUN || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
-	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4 && t->dec_units != 8 && t->dec_units != 16) || t->enc_nib < -1 || t->enc_nib > 1 ||
+	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||
 	    (t->size_order != 0 && t->size_order != 1) || t->enc_prefetch < 1 || t->enc_prefetch > 2 ||
 	    (t->enc_fused_waves_per_cu && (t->enc_fused_waves_per_cu < 3 || t->enc_fused_waves_per_cu > 32)) ||
-	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)))
+	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)) ||
+	    (t->dec_run_units != 1 && t->dec_run_units != 2 && t->dec_run_units != 4 && t->dec_run_units != 8 &&
+	     t->dec_run_units != 16))
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;

@@ -609,8 +609,9 @@ def test_slice_decode_matches(L, O, n, k, B, S):
         ids_np2[1, av[1, 1]] = ids_np2[1, av[1, 0]]
         ids_np2[2, :] = ids_np2[2, 0]
     outs = []
-    for kern, units in (("wave", 2), ("slice", 1), ("slice", 2), ("slice", 4), ("run", 1), ("run", 2), ("run", 4)):
-        with _tuned(dec_kernel=_dec(kern), dec_units=units):
+    for kern, units in (("wave", 2), ("slice", 1), ("slice", 2), ("slice", 4), ("run", 1), ("run", 2), ("run", 4),
+                        ("run", 16)):
+        with _tuned(dec_kernel=_dec(kern), dec_units=min(units, 4), dec_run_units=units):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             o, st = batch.decode(parts, n, dev(ids_np2), dev(np.ascontiguousarray(av)), k, B, out=out)
             torch.cuda.synchronize()
@@ -858,8 +859,8 @@ def test_bench_kernels_against_oracle(L, O, S, B):
         assert torch.equal(out, blocks[:, :B]), kern
 
 
-@pytest.mark.parametrize("n,k,waves,units", [(8, 5, 12, 2), (4, 2, 12, 2), (6, 3, 1, 4), (8, 8, 32, 1),
-                                             (5, 4, 2, 4), (3, 2, 32, 2)])
+@pytest.mark.parametrize("n,k,waves,units", [(8, 5, 12, 4), (4, 2, 12, 2), (6, 3, 1, 4), (8, 8, 32, 1),
+                                             (5, 4, 2, 8), (3, 2, 32, 2), (8, 5, 8, 16)])
 def test_run_decode_walks_across_stripes(L, O, n, k, waves, units):
     """The run decoder (nk8_walk.hip k_run_plan + k_decode_run): every
     resident wave walks one contiguous run of 1,024-row units across stripe
@@ -887,7 +888,7 @@ def test_run_decode_walks_across_stripes(L, O, n, k, waves, units):
         ids2[s, :] = ids2[s, 0]
     outs = []
     for kern in ("wave", "run"):
-        with _tuned(dec_kernel=_dec(kern), dec_units=units, dec_waves_per_cu=waves):
+        with _tuned(dec_kernel=_dec(kern), dec_run_units=units, dec_waves_per_cu=waves):
             out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
             st = batch.decode_ragged(parts, dev(poff), n, dev(ids2), dev(avail), k, out, dev(boff),
                                      dev(sizes.astype(np.int32)), int(sizes.max()))
@@ -907,7 +908,7 @@ def test_run_decode_walks_across_stripes(L, O, n, k, waves, units):
     uid = synth.batch_ids(S, n, first=77)
     up, _ = batch.encode(blocks, B, n, k, dev(uid))
     uav = dev(synth.batch_survivors(S, n, k, first=77))
-    with _tuned(dec_kernel=_dec("run"), dec_units=units, dec_waves_per_cu=waves):
+    with _tuned(dec_kernel=_dec("run"), dec_run_units=units, dec_waves_per_cu=waves):
         out, status = batch.decode(up, n, dev(uid), uav, k, B)
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0 and torch.equal(out, blocks[:, :B])

@@ -69,6 +69,19 @@ def main():
                 res.setdefault(path, []).append((enc_b / te / 1e9, dec_b / td / 1e9))
         torch.cuda.synchronize()
         ok = torch.equal(out, blocks[:, :B])
+        # every build's parts and digests against the first build's
+        ref = None
+        for path, L in libs:
+            pp = torch.zeros_like(parts)
+            dd = torch.zeros_like(dig)
+            _lib.check(L.nkfs_nk8_encode(blocks.data_ptr(), bpitch, B, S, n, k, ids.data_ptr(), pp.data_ptr(), pitch,
+                                         dd.data_ptr(), s))
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (pp[:, :ps], dd)
+            elif not (torch.equal(ref[0], pp[:, :ps]) and torch.equal(ref[1], dd)):
+                ok = False
+                print(f"{name} {path}: parts/digests differ from the first build")
         for path, r in res.items():
             e = sorted(x[0] for x in r)
             d = sorted(x[1] for x in r)
