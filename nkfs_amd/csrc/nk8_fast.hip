@@ -354,16 +354,18 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // warp-specialised kernel (4 encoder waves + 1 hash wave per 2 stripes)
     // wins: N8K5 1 MiB x 3,840: fused 3.60 / nibble 4.60 / warp-specialised
     // 4.90 TB/s, x 4,096: 3.84 / 4.76 / 5.06 (profiles/r01/ab_ws_shapes.txt).
-    // Small parts end each stripe's hash wave soon after its table build, so
-    // the rule wants 32 KiB parts (2,048 x 64 KiB, 13 KB parts: fused 3.76,
-    // warp-specialised 3.36 TB/s; ab_ws_rule.txt).  Ragged batches (sizes
-    // only on the device) keep the fused kernel.
+    // Ragged batches (sizes only on the device) keep the fused kernel.
     const u32 fused_waves = (g->nstripes + (E == 4 ? 3u : 1u)) / (E == 4 ? 4u : 2u);
     const u32 ps = g->block_sizes ? 0u : (g->block_size + u32(g->k) - 1) / u32(g->k);
-    // 1 MiB stripes take it at any grid size (C3 8,192 x 1 MiB: 4.94 ->
-    // 5.13 TB/s), 256 KiB ones only in small grids (C4 16,384 x 256 KiB:
-    // nibble-table fused 5.00, warp-specialised 4.76; profiles/r02/ab_c3_c4_enc.txt)
-    if (rules && E == 8 && digests && ps >= 32768 && (fused_waves <= 2048 || ps >= 131072))
+    // n > 4: parts of 8 KiB and up that the walk rule (walk_by_rule,
+    // nk8_kernels.hip) left here -- parts of 64 KiB and up, or grids too small
+    // for the walk encoder -- take the warp-specialised kernel: 256 x 64 KiB
+    // N8K5 ws 1,402 / walk 1,036 / fused 598 GB/s, C3 8,192 x 1 MiB ws 5,215
+    // / fused 5,023 (profiles/r03/seam_sweep_box1.txt).  n <= 4: parts of 8
+    // KiB and up, or at most 1,024 stripes: N4K2 65,536 x 16 KiB ws 5,816 /
+    // fused 4,960, 1,024 x 64 KiB 4,206 / 1,616, 1,024 x 4 KiB 1,336 / 911;
+    // C2 (65,536 x 4 KiB) stays fused 5,237 / ws 4,332 (seam_sweep_box2.txt).
+    if (rules && digests && (ps >= 8192 || (E == 4 && !g->block_sizes && g->nstripes <= 1024)))
         return nkfs_ws_encode(g, ids, digests, 4, false, st);
     // Nibble tables free LDS (N8K5: 25 -> 11 KB per wave, the occupancy
     // limit) at twice the lookups: a win where the grid offers more waves
@@ -763,6 +765,11 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     }
 }
 
+// stripes per wave of the wave decoder for k <= 4 (A/B builds: -DNKFS_DEC_G=2)
+#ifndef NKFS_DEC_G
+#define NKFS_DEC_G 1
+#endif
+
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
                                 int navail, int32_t *status, const void *gf, hipStream_t st,
                                 const uint64_t *expect, uint64_t *badmask)
@@ -777,7 +784,7 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     const GfTables *t = (const GfTables *)gf;
     const bool nt = false;
     const bool verify = expect != nullptr;
-    const int G = 1;
+    const int G = g->k <= 4 ? NKFS_DEC_G : 1;
     const u32 groups = (g->nstripes + G - 1) / G;
     // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4
     // steps; the verifying form hashes each part in order: one slice
@@ -808,9 +815,9 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
                                badmask);                                                                          \
     } while (0)
     switch (g->k) {
-    case 2: NKFS_DK(2, 4, 1); break;
-    case 3: NKFS_DK(3, 4, 1); break;
-    case 4: NKFS_DK(4, 4, 1); break;
+    case 2: NKFS_DK(2, 4, NKFS_DEC_G); break;
+    case 3: NKFS_DK(3, 4, NKFS_DEC_G); break;
+    case 4: NKFS_DK(4, 4, NKFS_DEC_G); break;
     case 5: NKFS_DK(5, 8, 1); break;
     case 6: NKFS_DK(6, 8, 1); break;
     case 7: NKFS_DK(7, 8, 1); break;

@@ -605,14 +605,19 @@ extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const u8 *ids, c
 // where one stripe is one chunk).
 static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
 {
-    // uniform n > 4 batches of 32-128 KiB parts on grids beyond 2,048 fused
-    // waves (C4: 16,384 x 256 KiB): the walk encoder, 4.75-4.93 -> 4.89-5.14
-    // TB/s across boxes (profiles/r02/ab_experiments.txt); 1 MiB stripes stay
-    // on the warp-specialised kernel (C3: walk 4.99-5.03, ws 5.08-5.15)
+    // uniform n > 4 batches: the walk encoder, except parts of 64 KiB and up,
+    // parts of 32 KiB and up on at most 1,024 stripes and parts of 8 KiB and
+    // up on at most 256 stripes, which take the warp-specialised kernel
+    // (nkfs_fast_encode).  Round-3 seam sweep, N8K5 (profiles/r03/
+    // seam_sweep_box{1,2}.txt): 1,024 x 64 KiB walk 3,502 / fused 2,211 / ws
+    // 3,045 GB/s; 65,536 x 4 KiB walk 3,027 / fused 2,669; 2,048 x 256 KiB
+    // walk 4,373 / ws 4,263; 256 x 64 KiB ws 1,552 / walk 1,111; 16,384 x
+    // 512 KiB ws 4,964 / walk 4,881.
     if (g->block_sizes || !digests || g->n <= 4)
         return 0;
     const u32 ps = (g->block_size + u32(g->k) - 1) / u32(g->k);
-    return ps >= 32768 && ps < 131072 && (g->nstripes + 1) / 2 > 2048;
+    const bool ws = ps >= 65536 || (ps >= 32768 && g->nstripes <= 1024) || (ps >= 8192 && g->nstripes <= 256);
+    return !ws;
 }
 
 static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStream_t st)
@@ -719,8 +724,13 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // in-wave inverse saves the plan launch
         // ragged batches with k >= 3: the run decoder (no per-slice metadata
         // chain, no setup scan; C5 decode +6 % over the ragged slice grid)
+        // k = 2: the wave decoder's in-wave inverse saves the plan launch on
+        // small stripes; from 32 KiB parts the slice grid wins (N4K2 65,536 x
+        // 256 KiB slice 5,636 / wave 5,314 GB/s, 1,024 x 256 KiB 4,962 /
+        // 4,551; C2's 4 KiB: 4,847 / 5,256; profiles/r03/seam_sweep_box2.txt)
+        const bool small_k2 = g->k < 3 && (g->block_sizes || part_size_of(g->block_size, g->k) < 32768);
         const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel
-                         : g->k < 3                    ? NKFS_DEC_WAVE
+                         : small_k2                    ? NKFS_DEC_WAVE
                          : g->block_sizes              ? NKFS_DEC_RUN
                                                        : NKFS_DEC_SLICE;
         if (kern == NKFS_DEC_RUN && !expect)

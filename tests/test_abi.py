@@ -102,3 +102,19 @@ def test_walk_offset_bound():
     # a stripe's part span and the block reach
     assert f(4096, (1 << 31), 1, 8) == 0
     assert f((1 << 31) - 2048 * 8, 16, 1, 2) == 0
+
+
+def test_decode_workspace_covers_every_plan_layout():
+    """nkfs_decode_workspace(nstripes, k) holds the k + k*k plan bytes per
+    stripe of the slice / general decoders and the run decoder's layout
+    (plans at a dword stride, then a u32 chunk prefix per stripe and a u32
+    total per 256-stripe group, each region 16-byte aligned)."""
+    L = _lib.lib()
+    for S in (1, 7, 255, 256, 257, 11520, 65536):
+        for k in (2, 3, 5, 8, 12, 32, 254):
+            w = L.nkfs_decode_workspace(S, k)
+            assert w >= S * (k + k * k)
+            stride = (k + k * k + 3) & ~3
+            loc = (S * stride + 15) & ~15
+            gsum = (loc + 4 * S + 15) & ~15
+            assert w >= gsum + 4 * ((S + 255) // 256), (S, k)

@@ -29,13 +29,14 @@ def main():
     quick = "--quick" in sys.argv
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(0))
-    n, k = 8, 5
-    sizes = [65536, 131072, 262144, 524288, 1048576]
-    counts = [256, 1024, 2048, 4096, 8192, 16384] if not quick else [1024, 4096]
-    print(f"{'S':>6} {'B':>8} {'ps':>7} {'fused_waves':>11} | encode GB/s: " + " ".join(f"{e:>6}" for e in ENC)
+    shapes = [(8, 5, B, S) for B in (65536, 131072, 262144, 524288, 1048576)
+              for S in ((256, 1024, 2048, 4096, 8192, 16384) if not quick else (1024, 4096))]
+    shapes += [(4, 2, B, S) for B in (4096, 16384, 65536, 262144) for S in (1024, 8192, 65536)]
+    shapes += [(8, 5, B, S) for B in (4096, 20480) for S in (1024, 8192, 65536)]
+    rounds = int(os.environ.get("SWEEP_ROUNDS", "3"))
+    print(f"{'n':>2} {'k':>2} {'S':>6} {'B':>8} {'ps':>7} {'fused_waves':>11} | encode GB/s: " + " ".join(f"{e:>6}" for e in ENC)
           + " | decode GB/s: " + " ".join(f"{d:>6}" for d in DEC), flush=True)
-    for B in sizes:
-        for S in counts:
+    for n, k, B, S in shapes:
             if S * B > (16 << 30):
                 continue
             ps = batch.part_size(B, k)
@@ -61,20 +62,27 @@ def main():
                                              out.data_ptr(), B, S, work.data_ptr(), st.data_ptr(), s))
 
             reps = 5 if S * B <= (4 << 30) else 3
-            er, dr, ref, ok = [], [], None, True
-            for name, tune in ENC.items():
-                with _lib.tuned(**tune):
-                    er.append(enc_b / timeit(enc, reps) / 1e9)
-                    torch.cuda.synchronize()
-                    got = dig.clone()
-                    ref = got if ref is None else ref
-                    ok &= bool(torch.equal(got, ref))
-            for name, tune in DEC.items():
-                with _lib.tuned(**tune):
-                    dr.append(dec_b / timeit(dec, reps) / 1e9)
-                    torch.cuda.synchronize()
-                    ok &= bool(torch.equal(out, blocks[:, :B])) and int(st.abs().sum()) == 0
-            print(f"{S:>6} {B:>8} {ps:>7} {(S + 1) // 2:>11} | " + " ".join(f"{x:6.0f}" for x in er) + " |              "
+            # variants interleaved over `rounds` passes, median per variant
+            # (the first launches after the buffers are allocated run slow)
+            er = {e: [] for e in ENC}
+            dr = {d: [] for d in DEC}
+            ref, ok = None, True
+            for _ in range(rounds):
+                for name, tune in ENC.items():
+                    with _lib.tuned(**tune):
+                        er[name].append(enc_b / timeit(enc, reps) / 1e9)
+                        torch.cuda.synchronize()
+                        got = dig.clone()
+                        ref = got if ref is None else ref
+                        ok &= bool(torch.equal(got, ref))
+                for name, tune in DEC.items():
+                    with _lib.tuned(**tune):
+                        dr[name].append(dec_b / timeit(dec, reps) / 1e9)
+                        torch.cuda.synchronize()
+                        ok &= bool(torch.equal(out, blocks[:, :B])) and int(st.abs().sum()) == 0
+            er = [sorted(v)[len(v) // 2] for v in er.values()]
+            dr = [sorted(v)[len(v) // 2] for v in dr.values()]
+            print(f"{n:>2} {k:>2} {S:>6} {B:>8} {ps:>7} {(S + 1) // 2:>11} | " + " ".join(f"{x:6.0f}" for x in er) + " |              "
                   + " ".join(f"{x:6.0f}" for x in dr) + f"  ok={ok}", flush=True)
             del blocks, parts, out, dig, work
             torch.cuda.empty_cache()
