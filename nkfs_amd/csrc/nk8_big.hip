@@ -46,8 +46,6 @@
 using namespace nkfs;
 using namespace nkfs::dev;
 
-typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-
 namespace {
 
 
@@ -210,196 +208,6 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     // dword writes), read back as 4 rows x 4 parts (ds_read_b128), 4x4 byte
     // transpose, one dword of 4 rows per part: wave w stores parts
     // 4w..4w+3, 64 lanes x 4 B = 256 contiguous bytes per instruction
-    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
-#pragma unroll
-    for (int t = 0; t < ENC_T; ++t) {
-        const u32 rt = r_begin + u32(t) * 256u;
-        if (rt >= v.ps)
-            break;  // workgroup-uniform
-        __syncthreads();
-        stage[0 * 256 + tid] = acc[t].x;
-        stage[1 * 256 + tid] = acc[t].y;
-        stage[2 * 256 + tid] = acc[t].z;
-        stage[3 * 256 + tid] = acc[t].w;
-        __syncthreads();
-        const uint4 q4 = *reinterpret_cast<const uint4 *>(stage + wave * 256 + 4 * lane);
-        u32 o[4];
-        transpose4(q4.x, q4.y, q4.z, q4.w, o[0], o[1], o[2], o[3]);
-        const u32 rr = rt + 4u * u32(lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int e = 4 * wave + j;
-            if (e < np && rr < v.ps) {
-                u8 *dst = v.parts + u64(p0 + e) * v.pitch + rr;
-                if (pal && rr + 4u <= v.ps) {
-                    *reinterpret_cast<u32 *>(dst) = o[j];
-                } else {
-                    for (u32 c = 0; c < 4 && rr + c < v.ps; ++c)
-                        dst[c] = u8(o[j] >> (8 * c));
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Nibble-table form (bank-conflict-free lookups).  A byte table U_j[x] read
-// by ds_read_b128 puts each 16-lane group's lanes on the 16 16-byte slots of
-// a 256-byte bank row by the low nibble of their data byte: random data
-// collides (measured conflict share 61 % encode, 85 % decode).  Here
-// U_j[x] = L_j[x & 15] ^ H_j[x >> 4], and each 16-entry table is stored
-// once per slot: entry e of table t for slot q at ((t*16 + e)*256 + q*16),
-// lane l reading slot l & 15 -- the 16 lanes of every ds_read_b128 group
-// have distinct l & 15, so every lookup is one LDS cycle per group.  Two
-// lookups per byte instead of one, 8 columns (16 tables, 64 KiB) per chunk.
-constexpr int NCOL = 8;  // columns per nibble-table chunk
-
-// The chunk's 16 nibble tables from its 8 coefficient rows: thread t writes
-// entry t >> 4 of every table for slot t & 15 (one ds_write_b128 each).
-__device__ inline void build_nib_tables(u8 *tbl, const uint4 *rows, int tid)
-{
-    const u32 e = u32(tid) >> 4, q = u32(tid) & 15u;
-#pragma unroll 1
-    for (int j = 0; j < NCOL; ++j) {
-        const uint4 c = rows[j];
-        const u32 row[4] = {c.x, c.y, c.z, c.w};
-        u32 basis[8][4];
-        make_basis<4>(basis, row);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            u32 v[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const u32 m = 0u - ((e >> i) & 1u);
-#pragma unroll
-                for (int w = 0; w < 4; ++w)
-                    v[w] ^= basis[4 * h + i][w] & m;
-            }
-            *reinterpret_cast<uint4 *>(tbl + ((2 * j + h) * 16 + e) * 256 + q * 16) = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-    }
-}
-
-// XOR of column j's term for data byte `byte` (slot base folded into t)
-__device__ __forceinline__ void nib_term(uint4 &acc, const u8 *t, int j, u32 byte)
-{
-    const uint4 a = *reinterpret_cast<const uint4 *>(t + j * 8192 + ((byte & 15u) << 8));
-    const uint4 b = *reinterpret_cast<const uint4 *>(t + j * 8192 + 4096 + ((byte & 0xF0u) << 4));
-    acc.x ^= a.x ^ b.x;
-    acc.y ^= a.y ^ b.y;
-    acc.z ^= a.z ^ b.z;
-    acc.w ^= a.w ^ b.w;
-}
-
-__global__ __launch_bounds__(256, 2) void k_encode_big_nib(nkfs_geom g, const u8 *ids, const GfTables *gft,
-                                                           u32 ngroups, u32 nslices)
-{
-    __shared__ __attribute__((aligned(16))) u8 tbl[2 * NCOL * 16 * 256];  // 64 KiB
-    __shared__ __attribute__((aligned(16))) u32 stage[4 * 256];           // [part quad][row]
-    __shared__ __attribute__((aligned(16))) uint4 coef[256];              // coef[m] = (x_{p0+e}^m), e < 16
-    __shared__ uint16_t glog[256];
-    __shared__ u8 gexp[256];
-
-    const u32 b = blockIdx.x;
-    const u32 loc = b >> 3;
-    const u32 grp = loc % ngroups;
-    const u32 slice = (loc / ngroups) % nslices;
-    const u32 s = (loc / ngroups / nslices) * 8 + (b & 7);
-    if (s >= g.nstripes)
-        return;
-    const Stripe v = stripe_at(g, s);
-    const u32 r_begin = slice * ENC_ROWS;
-    if (r_begin >= v.ps)
-        return;
-    const int n = g.n, k = g.k;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int p0 = int(grp) * 16, np = min(16, n - p0);
-
-    glog[tid] = gft->log[tid];
-    gexp[tid] = gft->exp[tid];
-    __syncthreads();
-    {
-        const u8 *sid = ids + u64(s) * u64(n) + p0;
-        u32 xs[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e)
-            xs[e] = e < np ? sid[e] : 0u;
-        const int kk = (k + NCOL - 1) / NCOL * NCOL;  // columns past k: zero rows
-        for (int m = tid; m < kk; m += 256) {
-            u32 w[4] = {0, 0, 0, 0};
-            if (m < k)
-#pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    if (e < np)
-                        w[e >> 2] |= gf_pow(glog, gexp, xs[e], u32(m)) << (8 * (e & 3));
-            coef[m] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-    }
-
-    const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
-    const __amdgpu_buffer_rsrc_t rs = brsrc(v.blk - mis, (v.B + mis + 3u) & ~3u);
-    const u8 *tl = tbl + (lane & 15) * 16;  // this lane's slot
-
-    uint4 acc[ENC_T];
-#pragma unroll
-    for (int t = 0; t < ENC_T; ++t)
-        acc[t] = make_uint4(0, 0, 0, 0);
-
-    const int nch = (k + NCOL - 1) / NCOL;
-    for (int cc = 0; cc < nch; ++cc) {
-        __syncthreads();  // coef[] written / the previous chunk's lookups done
-        build_nib_tables(tbl, coef + NCOL * cc, tid);
-        __syncthreads();
-        const bool tail = (u64(r_begin) + ENC_ROWS) * u64(k) > u64(v.B);
-        auto rows = [&](auto mask) {
-            constexpr bool MASK = decltype(mask)::value;
-            u32 tdep = 0;
-            auto load = [&](int t, u32 &x0, u32 &x1, u32 &x2, u32 &pos) {
-                const u32 r = r_begin + u32(t) * 256u + u32(tid);
-                pos = r * u32(k) + u32(NCOL) * u32(cc);  // block byte of column 8cc of row r
-                const u32 a = (pos + mis + tdep) & ~3u;
-                const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rs, a, 0, 0);
-                x0 = x.x;
-                x1 = x.y;
-                x2 = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 8u, 0, 0);
-            };
-            u32 c0, c1, c2, n0, n1, n2, posc, posn;
-            load(0, c0, c1, c2, posc);
-#pragma unroll
-            for (int t = 0; t < ENC_T; ++t) {
-                if (t + 1 < ENC_T)
-                    load(t + 1, n0, n1, n2, posn);
-                const u32 sh = (posc + mis) & 3u;
-                u32 d[2];
-                d[0] = __builtin_amdgcn_alignbyte(c1, c0, sh);
-                d[1] = __builtin_amdgcn_alignbyte(c2, c1, sh);
-                if constexpr (MASK) {
-                    const u32 valid = v.B > posc ? min(v.B - posc, 8u) : 0u;
-#pragma unroll
-                    for (int w = 0; w < 2; ++w) {
-                        const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
-                        d[w] &= u32((u64(1) << (8 * keep)) - 1u);
-                    }
-                }
-                uint4 e = acc[t];
-                const u8 *tt = tl + tdep;
-#pragma unroll
-                for (int j = 0; j < NCOL; ++j)
-                    nib_term(e, tt, j, (d[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-                acc[t] = e;
-                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
-                c0 = n0;
-                c1 = n1;
-                c2 = n2;
-                posc = posn;
-            }
-        };
-        if (tail)
-            rows(std::true_type{});
-        else
-            rows(std::false_type{});
-    }
-
     const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
 #pragma unroll
     for (int t = 0; t < ENC_T; ++t) {
@@ -640,13 +448,8 @@ extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const voi
     const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
-#if NKFS_BIG_NIB
-    hipLaunchKernelGGL(k_encode_big_nib, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
-                       u32(ngroups), u32(nslices ? nslices : 1));
-#else
     hipLaunchKernelGGL(k_encode_big, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
                        u32(ngroups), u32(nslices ? nslices : 1));
-#endif
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

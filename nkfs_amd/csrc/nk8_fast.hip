@@ -765,241 +765,6 @@ __global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, co
     }
 }
 
-// Persistent form of the wave decoder for small stripes (k <= 4, uniform,
-// no verify): one wave per resident slot walks stripes w, w + G, ...; the
-// next stripe's offered slots, their ids and its speculative part loads
-// (its first K offered slots) are issued while the current stripe is
-// selected, inverted and rebuilt, so the two dependent metadata loads and
-// the part loads of a stripe never stand alone on a wave's critical path.
-// Selection, inverse, tables and rows are the wave decoder's
-// (crt/nk8.c:446-599).
-template <int K, int E>
-__global__ __launch_bounds__(64) void k_decode_stream(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                      int navail, int32_t *status, const u8 *inv)
-{
-    constexpr int U = 2;
-    constexpr int W = E / 4;
-    constexpr int TB = 256 * E;
-    constexpr u32 R = 1024;  // rows per unit (16 per lane)
-    static_assert(E == 4, "k <= 4");
-    __shared__ __attribute__((aligned(16))) u8 tbl[K * TB];
-    __shared__ u8 slot[K], M[K + 1], xs[K], wrow[K][K];
-    __shared__ u8 cid_l[64], csl_l[64];
-    __shared__ u32 inv4[64];
-    __shared__ int have;
-
-    const int li = threadIdx.x;
-    inv4[li] = reinterpret_cast<const u32 *>(inv)[li];
-    const u32 B = g.block_size;
-    const u32 ps = part_size_of(B, K);
-    const u64 ppitch = g.part_pitch;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(g.blocks) | g.block_pitch) & 15) == 0;
-    const bool cl = li < navail;
-
-    u32 s = blockIdx.x;
-    if (s >= g.nstripes)
-        return;
-    auto slot_of = [&](u32 st) -> u32 { return cl ? u32(avail[u64(st) * navail + li]) : 0u; };
-    auto id_of = [&](u32 st, u32 sl) -> u32 { return cl ? u32(ids[u64(st) * n_slots + sl]) : 0u; };
-    auto load = [&](u32 st, const u32 (&sl)[K], u32 r0, u32 (&pv)[U][K][4]) {
-        const u8 *pb = g.parts + u64(st) * n_slots * ppitch;
-#pragma unroll
-        for (int uu = 0; uu < U; ++uu) {
-            const u32 r = r0 + uu * R + 16 * li;
-            if (r < ps)
-#pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    const uint4 t = *reinterpret_cast<const uint4 *>(pb + sl[c] * ppitch + r);  // pitch >= round16(ps)
-                    pv[uu][c][0] = t.x;
-                    pv[uu][c][1] = t.y;
-                    pv[uu][c][2] = t.z;
-                    pv[uu][c][3] = t.w;
-                }
-        }
-    };
-    auto spec_of = [&](u32 csl, u32 (&sp)[K]) {
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            sp[c] = c < navail ? u32(__shfl(int(csl), c, 64)) : 0u;
-    };
-
-    u32 csl = slot_of(s);
-    u32 cid = id_of(s, csl);
-    u32 spec[K];
-    spec_of(csl, spec);
-    u32 pv[U][K][4];
-    load(s, spec, 0, pv);
-    for (;;) {
-        const u32 sn = s + gridDim.x;
-        const bool more = sn < g.nstripes;
-        // the next stripe's offered slots: in flight from here
-        const u32 nsl = more ? slot_of(sn) : 0u;
-
-        // first K distinct ids in offered order (crt/nk8.c:512-537)
-        if (cl) {
-            csl_l[li] = u8(csl);
-            cid_l[li] = u8(cid);
-        }
-        __syncthreads();
-        if (navail <= 64) {
-            bool dup = false;
-            for (int j = 0; cl && j < li; ++j)
-                dup |= cid_l[j] == u8(cid);
-            const bool first = cl && !dup;
-            const u64 taken = u64(__ballot(first));
-            const int rank = __popcll(taken & ((1ull << li) - 1));
-            if (first && rank < K) {
-                xs[rank] = u8(cid);
-                slot[rank] = u8(csl);
-            }
-            if (li == 0) {
-                const int h = min(K, __popcll(taken));
-                have = h;
-                if (status)
-                    status[s] = h < K ? -EINVAL : 0;
-            }
-        }
-        __syncthreads();
-        const bool ok = have == K;
-        if (li == 0 && ok) {  // M(t) = prod_c (t + x_c)
-            u32 m[K + 1];
-            m[0] = 1;
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const u32 x = xs[c];
-                m[c + 1] = m[c];
-#pragma unroll
-                for (int i = c; i >= 1; --i)
-                    m[i] = m[i - 1] ^ gfm(x, m[i]);
-                m[0] = gfm(x, m[0]);
-            }
-#pragma unroll
-            for (int i = 0; i <= K; ++i)
-                M[i] = u8(m[i]);
-        }
-        __syncthreads();
-        if (ok && li < K) {  // row li of W = V^-1 (Lagrange basis)
-            const u32 xc = xs[li];
-            u32 q[K];
-            u32 acc = M[K];
-            q[K - 1] = acc;
-#pragma unroll
-            for (int i = K - 1; i >= 1; --i) {
-                acc = M[i] ^ gfm(xc, acc);
-                q[i - 1] = acc;
-            }
-            u32 d = 0;
-#pragma unroll
-            for (int i = K - 1; i >= 0; --i)
-                d = gfm(d, xc) ^ q[i];
-            const u32 dinv = (inv4[d >> 2] >> (8 * (d & 3))) & 0xFFu;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-                wrow[li][i] = u8(gfm(q[i], dinv));
-        }
-        __syncthreads();
-        if (ok) {
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                u32 rw[W];
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    u32 x = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (4 * w + b < K)
-                            x |= u32(wrow[c][4 * w + b]) << (8 * b);
-                    rw[w] = x;
-                }
-                u32 basis[8][W];
-                make_basis<W>(basis, rw);
-                build_table<W, 64>(tbl + c * TB, basis, li);
-            }
-        }
-        u32 sel[K];
-        bool respec = false;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            sel[c] = slot[c];
-            respec |= sel[c] != spec[c];
-        }
-        __syncthreads();
-        // the next stripe's ids and speculative part loads
-        const u32 nid = more ? id_of(sn, nsl) : 0u;
-        u32 nspec[K];
-        spec_of(nsl, nspec);
-        u32 pvn[U][K][4];
-        if (more)
-            load(sn, nspec, 0, pvn);
-        if (ok) {
-            u8 *out = const_cast<u8 *>(g.blocks) + u64(s) * g.block_pitch;
-            for (u32 r0 = 0; r0 < ps; r0 += U * R) {
-                if (r0 || respec)
-                    load(s, sel, r0, pv);  // a later step, or a selection past the first K offered
-#pragma unroll
-                for (int uu = 0; uu < U; ++uu) {
-                    const u32 rl = r0 + uu * R + 16 * li;
-                    if (rl >= ps)
-                        continue;
-                    u32 o[4 * K];
-                    u32 tdep = 0;
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        u32 row[4 * W];
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr) {
-                            const int r = 4 * gq + rr;
-                            row[rr * W] = 0;
-#pragma unroll
-                            for (int c = 0; c < K; ++c) {
-                                const u32 byte = (pv[uu][c][r >> 2] >> (8 * (r & 3))) & 0xFFu;
-                                row[rr * W] ^= *reinterpret_cast<const u32 *>(tbl + tdep + c * TB + byte * E);
-                            }
-                        }
-#pragma unroll
-                        for (int q = 0; q < K; ++q)
-                            o[gq * K + q] = pack_dword<K, W>(row, q);
-                    }
-                    const u64 off = u64(rl) * K;
-                    if (aligned && off + 16 * K <= B) {
-                        uint4 *dst = reinterpret_cast<uint4 *>(out + off);
-#pragma unroll
-                        for (int q = 0; q < K; ++q)
-                            store16(dst + q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3], false);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4 * K; ++q)
-                            for (int b = 0; b < 4; ++b)
-                                if (off + 4 * q + b < B)
-                                    out[off + 4 * q + b] = u8(o[q] >> (8 * b));
-                    }
-                }
-            }
-        }
-        if (!more)
-            return;
-        __syncthreads();  // this stripe's lookups are done before the next tables
-        s = sn;
-        csl = nsl;
-        cid = nid;
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            spec[c] = nspec[c];
-#pragma unroll
-        for (int uu = 0; uu < U; ++uu)
-#pragma unroll
-            for (int c = 0; c < K; ++c)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    pv[uu][c][q] = pvn[uu][c][q];
-    }
-}
-
-// stripes per wave of the wave decoder for k <= 4 (A/B builds: -DNKFS_DEC_G=2)
-#ifndef NKFS_DEC_G
-#define NKFS_DEC_G 1
-#endif
-
 extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
                                 int navail, int32_t *status, const void *gf, hipStream_t st,
                                 const uint64_t *expect, uint64_t *badmask)
@@ -1014,31 +779,7 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     const GfTables *t = (const GfTables *)gf;
     const bool nt = false;
     const bool verify = expect != nullptr;
-#if NKFS_DEC_STREAM
-    // small uniform stripes, k <= 4: the persistent form (one wave per
-    // resident slot, next stripe's metadata and parts in flight)
-    if (!verify && !g->block_sizes && g->k <= 4 && navail <= 64) {
-        int occ = 0;
-        const void *kf;
-        switch (g->k) {
-        case 2: kf = reinterpret_cast<const void *>(&k_decode_stream<2, 4>); break;
-        case 3: kf = reinterpret_cast<const void *>(&k_decode_stream<3, 4>); break;
-        default: kf = reinterpret_cast<const void *>(&k_decode_stream<4, 4>); break;
-        }
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kf, 64, 0) != hipSuccess || occ < 1)
-            occ = 8;
-        const int per = NKFS_DEC_STREAM > 1 && NKFS_DEC_STREAM < occ ? NKFS_DEC_STREAM : occ;
-        const u32 grid = u32(nkfs_cu_count()) * u32(per);
-        const dim3 gr(grid < g->nstripes ? grid : g->nstripes);
-        switch (g->k) {
-        case 2: hipLaunchKernelGGL((k_decode_stream<2, 4>), gr, dim3(64), 0, st, *g, n_slots, ids, avail, navail, status, t->inv); break;
-        case 3: hipLaunchKernelGGL((k_decode_stream<3, 4>), gr, dim3(64), 0, st, *g, n_slots, ids, avail, navail, status, t->inv); break;
-        default: hipLaunchKernelGGL((k_decode_stream<4, 4>), gr, dim3(64), 0, st, *g, n_slots, ids, avail, navail, status, t->inv); break;
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -EIO;
-    }
-#endif
-    const int G = g->k <= 4 ? NKFS_DEC_G : 1;
+    const int G = 1;
     const u32 groups = (g->nstripes + G - 1) / G;
     // enough waves to fill the chip (>= 4 per SIMD), never a slice under 4
     // steps; the verifying form hashes each part in order: one slice
@@ -1069,9 +810,9 @@ extern "C" int nkfs_fast_decode(const nkfs_geom *g, int n_slots, const uint8_t *
                                badmask);                                                                          \
     } while (0)
     switch (g->k) {
-    case 2: NKFS_DK(2, 4, NKFS_DEC_G); break;
-    case 3: NKFS_DK(3, 4, NKFS_DEC_G); break;
-    case 4: NKFS_DK(4, 4, NKFS_DEC_G); break;
+    case 2: NKFS_DK(2, 4, 1); break;
+    case 3: NKFS_DK(3, 4, 1); break;
+    case 4: NKFS_DK(4, 4, 1); break;
     case 5: NKFS_DK(5, 8, 1); break;
     case 6: NKFS_DK(6, 8, 1); break;
     case 7: NKFS_DK(7, 8, 1); break;

@@ -725,10 +725,11 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // ragged batches with k >= 3: the run decoder (no per-slice metadata
         // chain, no setup scan; C5 decode +6 % over the ragged slice grid)
         // k = 2: the wave decoder's in-wave inverse saves the plan launch on
-        // small stripes; from 32 KiB parts the slice grid wins (N4K2 65,536 x
+        // small stripes; from 64 KiB parts the slice grid wins (N4K2 65,536 x
         // 256 KiB slice 5,636 / wave 5,314 GB/s, 1,024 x 256 KiB 4,962 /
-        // 4,551; C2's 4 KiB: 4,847 / 5,256; profiles/r03/seam_sweep_box2.txt)
-        const bool small_k2 = g->k < 3 && (g->block_sizes || part_size_of(g->block_size, g->k) < 32768);
+        // 4,551; 1,024 x 64 KiB wave 5,412 / slice 4,584; C2's 4 KiB: 5,236
+        // / 4,796; profiles/r03/seam_sweep_box{2,3}.txt)
+        const bool small_k2 = g->k < 3 && (g->block_sizes || part_size_of(g->block_size, g->k) < 65536);
         const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel
                          : small_k2                    ? NKFS_DEC_WAVE
                          : g->block_sizes              ? NKFS_DEC_RUN
