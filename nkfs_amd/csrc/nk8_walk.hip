@@ -199,6 +199,9 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
         par0 = g.parts;
     }
     const u32 ps = part_size_of(B, K);
+    if constexpr (RAGGED)  // part-size window of this launch (whole wave)
+        if ((g.part_min && ps < g.part_min) || (g.part_max && ps >= g.part_max))
+            return;
     const u32 nch = (ps + R - 1) / R;
     const u32 ntask = per_wave * nch;
     auto stripe_of = [&](u32 j) { return RAGGED ? s0 : s0 + j * grid; };
@@ -895,7 +898,7 @@ static int launch_walk_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *id
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, int units, int nib,
                                 int waves, int cus, hipStream_t st)
 {
-    if (g->n > 8 || g->k > 8 || g->part_min || g->part_max)
+    if (g->n > 8 || g->k > 8 || (!g->block_sizes && (g->part_min || g->part_max)))
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
