@@ -626,21 +626,6 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
     const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
                      : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
                                                                   : NKFS_ENC_AUTO;
-#if NKFS_RAGGED_SPLIT
-    // ragged n > 4 batches with digests: stripes with parts of at least
-    // NKFS_RAGGED_SPLIT bytes on the warp-specialised kernel, the rest on
-    // the walk encoder (two launches over complementary part-size windows)
-    if (t.enc_kernel == NKFS_ENC_AUTO && g->block_sizes && digests && g->n > 4 && !g->part_min && !g->part_max) {
-        nkfs_geom big = *g, small = *g;
-        big.part_min = NKFS_RAGGED_SPLIT;
-        small.part_max = NKFS_RAGGED_SPLIT;
-        int rc = nkfs_ws_encode(&big, ids, digests, 4, false, st);
-        if (!rc)
-            rc = nkfs_walk_encode(&small, ids, digests, 1, t.enc_nib < 0 ? 0 : t.enc_nib, t.enc_waves_per_cu,
-                                  nkfs_cu_count(), st);
-        return rc;
-    }
-#endif
     if (kern == NKFS_ENC_WALK) {
         // two 1,024-row units per chunk for n <= 4 (a 4 KiB N4K2 stripe is one chunk)
         const int units = g->n <= 4 ? (t.enc_units ? t.enc_units : 2) : 1;
