@@ -94,6 +94,14 @@ static uint64_t round16(uint64_t v) { return (v + 15) & ~(uint64_t)15; }
  * Block and ids go over in one copy from pinned staging, the n parts come
  * back in one copy (the per-call fixed cost is two copies, one launch and
  * one stream sync). */
+/* Blocks up to this size take the zero-copy form: the kernel reads the
+ * block from the pinned staging buffer and writes the parts back into it
+ * over PCIe, so a small call costs one launch and one sync instead of two
+ * DMA copies as well. */
+#ifndef NKFS_ZC_MAX
+#define NKFS_ZC_MAX 1048576
+#endif
+
 static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8_t *ids, uint8_t **parts)
 {
 	struct nkfs_ctx *c = nkfs_ctx_get();
@@ -105,6 +113,21 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 	uint64_t off_ids = round16(B), off_parts = off_ids + round16((uint64_t)n);
 	uint64_t in_bytes = off_parts, parts_bytes = pitch * (uint64_t)n;
 	void *dv, *hv;
+	if (B <= NKFS_ZC_MAX) {
+		if ((err = nkfs_ctx_host(c, off_parts + parts_bytes, &hv)))
+			goto out;
+		uint8_t *h = hv;
+		memcpy(h, block, B);
+		memcpy(h + off_ids, ids, (size_t)n);
+		struct nkfs_geom zg = { h, round16(B), B, NULL, NULL, h + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0 };
+		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)))
+			goto out;
+		HIPGO(hipStreamSynchronize(c->stream));
+		for (int i = 0; i < n; i++)
+			memcpy(parts[i], h + off_parts + pitch * (uint64_t)i, ps);
+		err = 0;
+		goto out;
+	}
 	if ((err = nkfs_ctx_dev(c, off_parts + parts_bytes, &dv)) ||
 	    (err = nkfs_ctx_host(c, in_bytes > parts_bytes ? in_bytes : parts_bytes, &hv)))
 		goto out;
@@ -193,6 +216,30 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 	uint64_t off_block = off_status + 16;
 	uint64_t in_bytes = off_work, out_bytes = 16 + round16(block_size);
 	void *dv, *hv;
+	if (block_size <= NKFS_ZC_MAX) {
+		/* zero-copy: the decode reads the parts from pinned staging and
+		 * writes status and block back into it (layout as the device's) */
+		if ((err = nkfs_ctx_host(c, off_block + round16(block_size), &hv)))
+			goto out;
+		uint8_t *h = hv;
+		for (int c2 = 0; c2 < k; c2++) {
+			memcpy(h + off_parts + pitch * (uint64_t)c2, parts[sel[c2]], ps);
+			h[off_ids + c2] = ids[sel[c2]];
+			h[off_avail + c2] = (uint8_t)c2;
+		}
+		struct nkfs_geom zg = { h + off_block, round16(block_size), block_size, NULL, NULL, h + off_parts, pitch,
+					NULL, 1, k, k, NULL, 0, 0 };
+		if ((err = nkfs_launch_decode(&zg, k, h + off_ids, h + off_avail, k, h + off_work,
+					      (int32_t *)(h + off_status), nkfs_gf(), c->stream, NULL, NULL)))
+			goto out;
+		HIPGO(hipStreamSynchronize(c->stream));
+		int32_t zst;
+		memcpy(&zst, h + off_status, sizeof(zst));
+		if (!zst)
+			memcpy(block, h + off_block, block_size);
+		err = zst;
+		goto out;
+	}
 	if ((err = nkfs_ctx_dev(c, off_block + round16(block_size), &dv)) ||
 	    (err = nkfs_ctx_host(c, in_bytes > out_bytes ? in_bytes : out_bytes, &hv)))
 		goto out;

@@ -647,7 +647,7 @@ static bool few_big_stripes(const nkfs_geom *g)
 {
     const u32 ps = max_part_size(g, g->block_size);
     return !g->block_sizes && nkfs_tune_now().enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
-           g->nstripes < 64 && ps >= 8192;
+           g->nstripes < 64 && ps >= 1024;
 }
 
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
