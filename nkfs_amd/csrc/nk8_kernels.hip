@@ -730,10 +730,14 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // 4,551; 1,024 x 64 KiB wave 5,412 / slice 4,584; C2's 4 KiB: 5,236
         // / 4,796; profiles/r03/seam_sweep_box{2,3}.txt)
         const bool small_k2 = g->k < 3 && (g->block_sizes || part_size_of(g->block_size, g->k) < 65536);
-        const int kern = t.dec_kernel != NKFS_DEC_AUTO ? t.dec_kernel
-                         : small_k2                    ? NKFS_DEC_WAVE
-                         : g->block_sizes              ? NKFS_DEC_RUN
-                                                       : NKFS_DEC_SLICE;
+        // ragged: the run decoder on batches that give its persistent grid
+        // several chunks per wave; the host pipeline's sub-batches (tens of
+        // stripes) keep the slice grid (C5 GET from host memory: run 20.7,
+        // slice 31.6 GiB/s; profiles/r03/pcie.txt)
+        const int kern = t.dec_kernel != NKFS_DEC_AUTO         ? t.dec_kernel
+                         : small_k2                            ? NKFS_DEC_WAVE
+                         : g->block_sizes && g->nstripes >= 2048 ? NKFS_DEC_RUN
+                                                                 : NKFS_DEC_SLICE;
         if (kern == NKFS_DEC_RUN && !expect)
             rc = nkfs_run_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_run_units, t.dec_waves_per_cu,
                                  nkfs_cu_count(), st);

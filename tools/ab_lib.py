@@ -42,7 +42,10 @@ def main():
     libs = [(p, load(p)) for p in sys.argv[1:] if p.endswith(".so")]
     batch.gpu_init(0)  # the in-tree build synthesises the inputs
     for name in [a for a in sys.argv[1:] if not a.endswith(".so")]:
-        S, B, n, k, _ = CONFIGS[name]
+        if name in CONFIGS:
+            S, B, n, k, _ = CONFIGS[name]
+        else:  # S:B:n:k
+            S, B, n, k = (int(x) for x in name.split(":"))
         ps = batch.part_size(B, k)
         # layout experiments: AB_PPAD / AB_BPAD bytes added to the part / block pitch
         pitch = batch.part_pitch(B, k) + int(os.environ.get("AB_PPAD", "0"))
