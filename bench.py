@@ -122,6 +122,24 @@ def byte_balanced_ranges(sizes, world: int):
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def rank_spread(enc_s: float, dec_s: float, device) -> dict:
+    """Every rank's mean encode / decode launch time (µs), all-gathered, so
+    that a line at N > 1 shows the imbalance between ranks (max and min next
+    to the per-rank list; the headline's roofline is rank 0's launches)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([enc_s * 1e6, dec_s * 1e6], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        out = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, v)
+    else:
+        out = [v]
+    enc = [round(float(t[0]), 2) for t in out]
+    dec = [round(float(t[1]), 2) for t in out]
+    return {"encode_us": enc, "decode_us": dec, "encode_us_max": max(enc), "encode_us_min": min(enc),
+            "decode_us_max": max(dec), "decode_us_min": min(dec)}
+
+
 def reduce_max(value: float, device) -> float:
     import torch
     import torch.distributed as dist
@@ -288,11 +306,56 @@ def box_stream(src, dst, read_bytes, write_bytes, stream):
     return {"GBps": round(best, 1), "read_write_kib": [L, S], "frac_of_peak": round(best / HBM_PEAK_GBS, 4)}
 
 
+_ANCHOR = {}
+
+
+def hbm_anchor(src, dst, stream):
+    """The microarch guide's own anchor (MI355X_MICROARCH.md: 6.29 TB/s
+    measured for a float4 copy), measured once per process on this box:
+    plain grid-stride float4 copy, pure read and pure write kernels
+    (boxprobe.hip nkfs_probe_plain), best of three grid sizes, over up to 4
+    GiB of the headline's own buffers (past the 256 MB Infinity Cache).  It
+    anchors `box_stream` independently of the product's access shape."""
+    import ctypes as C
+    if _ANCHOR:
+        return _ANCHOR
+    P = probe_lib()
+    if P is None or not hasattr(P, "nkfs_probe_plain"):
+        return None
+    P.nkfs_probe_plain.restype = C.c_int
+    P.nkfs_probe_plain.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                   C.POINTER(C.c_float), C.POINTER(C.c_double)]
+    nbytes = min(src.numel() * src.element_size(), dst.numel() * dst.element_size(), 4 << 30) // 4096 * 4096
+    cus = 256
+    try:
+        import torch
+        cus = torch.cuda.get_device_properties(src.device).multi_processor_count
+    except Exception:  # noqa: BLE001 -- property lookup only
+        pass
+    out = {"bytes_per_buffer": nbytes}
+    for kind, name in ((0, "copy"), (1, "read"), (2, "write")):
+        best, best_grid = 0.0, 0
+        for per_cu in (4, 8, 32):
+            ms, moved = C.c_float(0), C.c_double(0)
+            rc = P.nkfs_probe_plain(src.data_ptr(), dst.data_ptr(), nbytes, kind, per_cu * cus, 7,
+                                    stream.cuda_stream, C.byref(ms), C.byref(moved))
+            if rc == 0 and ms.value > 0 and moved.value / (ms.value * 1e-3) / 1e9 > best:
+                best, best_grid = moved.value / (ms.value * 1e-3) / 1e9, per_cu
+        out[f"{name}_GBps"] = round(best, 1)
+        out[f"{name}_wg_per_cu"] = best_grid
+    out["kernel"] = "boxprobe.hip k_copy4/k_read4/k_write4: grid-stride float4, 256 threads/WG"
+    _ANCHOR.update(out)
+    return _ANCHOR
+
+
 def with_box(roof, box):
-    """Attach the box's own stream ceiling to a roofline dict."""
+    """Attach the box's own stream ceiling to a roofline dict, and the
+    kernel's fraction of the guide's plain float4 copy measured on this box."""
     if box:
         roof["box_stream"] = box
         roof["frac_of_box_stream"] = round(roof["achieved"] / box["GBps"], 4)
+    if _ANCHOR.get("copy_GBps"):
+        roof["frac_of_anchor_copy"] = round(roof["achieved"] / _ANCHOR["copy_GBps"], 4)
     return roof
 
 
@@ -311,7 +374,7 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
     import torch
     from nkfs_amd import batch, synth
     S, B, n, k, desc = CONFIGS[name]
-    head = f"{desc.split(', ')[0]}, {desc.split(', ')[1]}"
+    head = desc.split(", ")[0]  # "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased)"
     if strong_total:
         first, S = strong_range(rank, world, strong_total)
         desc = (f"{head}, {strong_total} x {B // 1024} KiB stripes in all, split evenly over {world} GPU(s) "
@@ -380,6 +443,7 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
     user_bytes = total_stripes * B * steps
     # the box's own ceiling for each kernel's read:write mix, on the
     # kernel's own buffers (after verification: the probe overwrites them)
+    hbm_anchor(blocks, parts, stream)
     box_enc = box_stream(blocks, parts, S * B, S * n * ps, stream)
     box_dec = box_stream(parts, out, S * k * ps, S * B, stream)
     dec = with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
@@ -396,8 +460,9 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
                                       pmc_traffic(name, S, world)), box_enc),
         "decode": dec,
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
+        "per_rank": rank_spread(enc_s, dec_s, device),
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:  # at every world size (rank 0's host cores)
         res["cpu_baseline"] = cpu_baseline(S, B, n, k, args.cpu_seconds)
     if rank == 0 and args.pcie:
         res["pcie_inclusive_GiBps"] = pcie_rate(batch, blocks, S, B, n, k, ids)
@@ -500,6 +565,7 @@ def run_ragged(args, rank, world, device, steps):
     enc_bytes = user + n * sum(ps) + 8 * n * S
     dec_bytes = k * sum(ps) + user + k * S
     total_user = reduce_sum(user, device)
+    hbm_anchor(blocks, parts, stream)
     box_enc = box_stream(blocks, parts, user, n * sum(ps), stream)
     box_dec = box_stream(parts, out, k * sum(ps), user, stream)
     res = {
@@ -510,13 +576,14 @@ def run_ragged(args, rank, world, device, steps):
                    "parallelism": f"stripe-partition x{world} (byte-balanced ranges)"},
         "scaling": "weak",
         "roofline": with_box(roofline("nkfs_nk8_encode_ragged (encode + XXH64 per part)", enc_bytes, enc_s,
-                                      pmc_traffic("c5", None, world)), box_enc),
+                                      pmc_traffic("c5", S, world)), box_enc),
         "decode": with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
                             "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4),
                             "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes}, box_dec),
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
+        "per_rank": rank_spread(enc_s, dec_s, device),
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:  # at every world size (rank 0's host cores)
         res["cpu_baseline"] = cpu_baseline_mixed(sizes, n, k, args.cpu_seconds)
     if rank == 0 and args.pcie:
         res["pcie_inclusive_GiBps"] = pcie_rate_ragged(batch, blocks, boff, poff, sizes, ids_np, n, k, ppos)
@@ -579,7 +646,9 @@ def main():
     if subs:
         result["configs"] = subs
         result["verified"] = bool(result["verified"]) and all(v["verified"] for v in subs.values())
-    if rank == 0 and not args.no_cpu and world == 1:
+    if _ANCHOR:
+        result["hbm_anchor"] = dict(_ANCHOR)
+    if rank == 0 and not args.no_cpu:
         result["cpu_model"] = cpu_model()
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -674,19 +743,21 @@ def pmc_traffic(config, stripes=None, world=1):
     """Per-launch HBM bytes of the encode kernel from the committed rocprofv3
     PMC summary (tools/pmc.sh: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
     FETCH_SIZE halving corrected per MI355X_MICROARCH.md §HBM), or None.
-    Attached only to a line whose per-GPU stripe count is the profiled
-    run's and that runs on one GPU (the PMC pass is a 1-GPU run)."""
-    if world != 1:
-        return None
+    A launch's traffic depends only on the batch one GPU holds, so an entry
+    is attached to any line -- at any world size -- whose per-GPU stripe
+    count is the profiled run's: "c3@1024" is the c3 kernel on 1,024
+    stripes (the N = 8 strong shard), "c3" the full 8,192."""
+    del world  # per-GPU traffic: the PMC pass of the same per-GPU batch on one GPU
     path = os.path.join(ROOT, "profiles", "traffic.json")
+    want = CONFIGS[config][0] if stripes is None else stripes
     try:
         with open(path) as f:
-            entry = json.load(f).get(config)
-        # measured on this config's own batch only (tools/pmc.sh records it)
-        want = CONFIGS[config][0] if stripes is None else stripes
-        if entry is None or entry.get("stripes") != want:
-            return None
-        return entry["encode_bytes_per_launch"]
+            doc = json.load(f)
+        for key in (f"{config}@{want}", config):
+            entry = doc.get(key)
+            if entry is not None and entry.get("stripes") == want:
+                return entry["encode_bytes_per_launch"]
+        return None
     except (OSError, ValueError, KeyError):
         return None
 

@@ -83,6 +83,7 @@ struct nkfs_tune {
 	int enc_fused_waves_per_cu; /* fused encoder: resident waves per CU cap (0 = none, 3..32) */
 	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
 	int dec_run_units;    /* run decoder: 1,024-row units per chunk (1, 2, 4, 8, 16) */
+	int enc_ws_prefetch;  /* warp-specialised encoder, n > 4: chunks of loads in flight per encoder wave (1, 2) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */
@@ -90,6 +91,14 @@ int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields;
  * bits (block bytes + a chunk's reach, a stripe's part span, the digest
  * array), else 0: the launcher then takes the general kernels. */
 int nkfs_walk_offsets_fit(uint64_t block_size, uint64_t part_span, uint64_t nstripes, uint64_t n);
+/* CPU-only replay of the plan a ragged host call (nkfs_nk8_encode_ragged_host
+ * / _decode_ragged_host, or the page-list forms when page_size > 0) makes:
+ * sub-batch cuts, device layout, shifted offsets; checks that every kernel
+ * access and copy of every sub-batch stays inside its region.  0 (msg: a
+ * summary), -ERANGE (msg: the first violation) or -EINVAL.  No GPU call. */
+int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *block_size, uint32_t max_block_size,
+			uint32_t nstripes, int n_slots, int k, int navail, const uint64_t *part_off, uint32_t page_size,
+			uint64_t chunk_bytes, char *msg, size_t msg_len);
 
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */
 uint32_t nkfs_part_size(uint32_t block_size, int k);

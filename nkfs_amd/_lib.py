@@ -14,7 +14,10 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libnkfs_crt.so")
+# NKFS_LIB: test tooling may point at another build of the same library
+# (nkfs_amd/lib/debug/libnkfs_crt.so, `make DEBUG_BOUNDS=1`); the product
+# path loads the in-tree build.
+LIB_PATH = os.environ.get("NKFS_LIB") or os.path.join(HERE, "lib", "libnkfs_crt.so")
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
@@ -31,7 +34,8 @@ class Tune(C.Structure):
     """struct nkfs_tune (include/nkfs_gpu.h): kernel choice and launch shape."""
     _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
                                        "dec_units", "enc_nib", "enc_units", "size_order", "enc_prefetch",
-                                       "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units")]
+                                       "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units",
+                                       "enc_ws_prefetch")]
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4, "wide": 5, "big": 6, "wide_ws": 7}
@@ -101,6 +105,8 @@ _SIGS = {
     "nkfs_memcpy_h2d": (C.c_int, [vp, vp, C.c_size_t]),
     "nkfs_memcpy_d2h": (C.c_int, [vp, vp, C.c_size_t]),
     "nkfs_stream_sync": (C.c_int, [vp]),
+    "nkfs_pipeline_check": (C.c_int, [C.c_int, vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, vp,
+                                      C.c_uint32, C.c_uint64, C.c_char_p, C.c_size_t]),
 }
 
 _lib = None

@@ -224,15 +224,22 @@ static int xh_complete(struct xh *h, uint32_t flags, const struct xstate *s, uin
 
 /* ------------------------------------------------------- pending slots */
 
-#define NSLOT 1024
+/* At most NSLOT messages are pending on the GPU at once (each holds a
+ * per-call context: a stream and 512 KiB of pinned staging); beyond that an
+ * update folds synchronously (one round trip), so a burst of states -- or
+ * states abandoned while pending (never digested, reset or freed), whose
+ * slot stays taken -- cannot pin more than NSLOT contexts. */
+#define NSLOT 64
 #define PEND_MAGIC 0xC5A10000u
+#define PEND_POISON (PEND_MAGIC | 0xFFFFu) /* a failed update: every later update / digest fails */
 
 struct xslot {
 	uint64_t token;
 	int used;
+	pthread_mutex_t mu; /* complete-and-free of this slot (concurrent digests of one state) */
 	struct xh h;
 };
-static struct xslot g_slot[NSLOT];
+static struct xslot g_slot[NSLOT] = { [0 ... NSLOT - 1] = { .mu = PTHREAD_MUTEX_INITIALIZER } };
 static pthread_mutex_t g_slot_lock = PTHREAD_MUTEX_INITIALIZER;
 static uint64_t g_token = 0x6E6B38465A5A0001ull;
 
@@ -241,12 +248,13 @@ static uint64_t g_token = 0x6E6B38465A5A0001ull;
 static struct xslot *slot_of(const struct xstate *s, int *stale)
 {
 	*stale = 0;
-	if ((s->pend & 0xFFFF0000u) != PEND_MAGIC)
+	const uint32_t pend = __atomic_load_n(&s->pend, __ATOMIC_ACQUIRE);
+	if ((pend & 0xFFFF0000u) != PEND_MAGIC)
 		return NULL;
-	const uint32_t i = s->pend & 0xFFFFu;
+	const uint32_t i = pend & 0xFFFFu;
 	struct xslot *sl = i < NSLOT ? &g_slot[i] : NULL;
 	pthread_mutex_lock(&g_slot_lock);
-	const int ok = sl && sl->used && sl->token == s->v[0];
+	const int ok = sl && sl->used && sl->token == __atomic_load_n(&s->v[0], __ATOMIC_RELAXED);
 	pthread_mutex_unlock(&g_slot_lock);
 	if (!ok) {
 		*stale = 1;
@@ -337,7 +345,7 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 		if (xh_begin(h, s->v)) {
 			if (sl)
 				slot_free(sl);
-			return XXH_ERROR;
+			return XXH_ERROR; /* nothing of the state changed yet */
 		}
 		if (sl) {
 			s->v[0] = sl->token;
@@ -366,10 +374,13 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 	if (h == &local)
 		xh_end(h);
 	if (err) {
-		if (h != &local) {
+		/* part of the input may already be folded or consumed from mem64:
+		 * the state no longer describes any prefix of the input, so poison
+		 * it -- every later update returns XXH_ERROR and a digest traps
+		 * (as CRT_BUG) instead of returning a wrong sum; reset clears it */
+		if (h != &local)
 			slot_free(sl);
-			s->pend = 0;
-		}
+		__atomic_store_n(&s->pend, PEND_POISON, __ATOMIC_RELEASE);
 		return XXH_ERROR;
 	}
 	p += nst * 32;
@@ -381,30 +392,47 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 	return XXH_OK;
 }
 
-/* returns 0 and fills *out, or a negative errno */
+/* returns 0 and fills *out, or a negative errno.  A pending message is
+ * completed and its slot freed under the slot's mutex, and the state is
+ * written back (accumulators, pend = 0) before the mutex is released: a
+ * second digest of the same state (the reference's digest is read-only, so
+ * callers may digest one state from two threads) then finds it no longer
+ * pending and finishes from the written-back accumulators. */
 static int finish(struct xstate *s, uint64_t *out)
 {
-	int stale;
-	struct xslot *sl = slot_of(s, &stale);
-	if (stale)
-		return -EINVAL;
-	if (!sl) { /* nothing on the GPU: merge + tail + avalanche in one launch */
-		struct xh h;
-		int err = xh_begin(&h, s->v);
-		if (!err)
-			err = xh_complete(&h, NKFS_XXH_FINISH, s, out, NULL);
-		xh_end(&h);
+	for (;;) {
+		int stale;
+		struct xslot *sl = slot_of(s, &stale);
+		if (stale)
+			return -EINVAL;
+		if (!sl) { /* nothing on the GPU: merge + tail + avalanche in one launch */
+			struct xh h;
+			uint64_t v0[4];
+			memcpy(v0, s->v, 32);
+			int err = xh_begin(&h, v0);
+			if (!err)
+				err = xh_complete(&h, NKFS_XXH_FINISH, s, out, NULL);
+			xh_end(&h);
+			return err;
+		}
+		pthread_mutex_lock(&sl->mu);
+		const uint32_t pend = __atomic_load_n(&s->pend, __ATOMIC_ACQUIRE);
+		pthread_mutex_lock(&g_slot_lock);
+		const int mine = pend == (PEND_MAGIC | (uint32_t)(sl - g_slot)) && sl->used && sl->token == s->v[0];
+		pthread_mutex_unlock(&g_slot_lock);
+		if (!mine) { /* another digest completed it meanwhile: look again */
+			pthread_mutex_unlock(&sl->mu);
+			continue;
+		}
+		uint64_t v[4];
+		int err = xh_complete(&sl->h, NKFS_XXH_FINISH | NKFS_XXH_EMIT, s, out, v);
+		if (!err) /* the state is now what the reference's is after the same updates */
+			memcpy(s->v, v, 32);
+		__atomic_store_n(&s->pend, err ? PEND_POISON : 0u, __ATOMIC_RELEASE);
+		slot_free(sl);
+		pthread_mutex_unlock(&sl->mu);
 		return err;
 	}
-	uint64_t v[4];
-	int err = xh_complete(&sl->h, NKFS_XXH_FINISH | NKFS_XXH_EMIT, s, out, v);
-	slot_free(sl);
-	s->pend = 0;
-	if (err)
-		return err;
-	/* the state is now what the reference's is after the same updates */
-	memcpy(s->v, v, 32);
-	return 0;
 }
 
 /* The reference returns a digest unconditionally; a GPU failure here has

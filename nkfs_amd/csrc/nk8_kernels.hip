@@ -11,9 +11,13 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "../../include/nkfs_gpu.h"
 #include "gf256.h"
 #include "nkfs_internal.h"
+#include "runtime.h"
+#include "scratch.h"
 #include "xxh64_dev.h"
 
 using namespace nkfs;
@@ -560,26 +564,83 @@ extern "C" int nkfs_launch_gf_init(void *gf, void *stream)
     return launch_ok();
 }
 
+// ---------------------------------------------------------------- scratch
+//
+// A launch's own metadata (the ragged size order, the ragged slice map)
+// lives in the caller's scratch when nkfs_geom.scratch provides it (the host
+// pipeline carves it from its context buffer), else in stream-ordered
+// allocations from a private per-device pool.  The private pool allows
+// reuse only along stream-ordered dependencies: opportunistic and
+// driver-inserted cross-stream reuse are off, so a block freed on one stream
+// never goes to another stream's allocation before the freeing work is
+// ordered before it (the default pool allows both; round-3 fault audit,
+// DESIGN.md §5.6).  Allocation stays stream-ordered, so calls remain
+// graph-capturable.
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pool[NKFS_MAX_DEVICES];
+
+extern "C" hipMemPool_t nkfs_private_pool(hipStream_t st)
+{
+    int dev = -1;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= NKFS_MAX_DEVICES)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool[dev])
+        return g_pool[dev];
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t p = nullptr;
+    if (hipMemPoolCreate(&p, &props) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    int off = 0, on = 1;
+    uint64_t keep = 64ull << 20;  // keep up to 64 MiB cached across syncs
+    if (hipMemPoolSetAttribute(p, hipMemPoolReuseAllowOpportunistic, &off) != hipSuccess ||
+        hipMemPoolSetAttribute(p, hipMemPoolReuseAllowInternalDependencies, &off) != hipSuccess ||
+        hipMemPoolSetAttribute(p, hipMemPoolReuseFollowEventDependencies, &on) != hipSuccess ||
+        hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipMemPoolDestroy(p);
+        return nullptr;
+    }
+    g_pool[dev] = p;
+    return p;
+}
+
+extern "C" uint64_t nkfs_ragged_scratch_bytes(uint32_t nstripes, uint64_t sum_units)
+{
+    const u64 perm = (u64(nstripes) * 4 + 255) & ~u64(255);
+    const u64 head = ((u64(nstripes) + 2) * 4 + 15) & ~u64(15);
+    return perm + ((head + sum_units * 8 + 255) & ~u64(255));
+}
+
 // ragged batches pass the bound on block sizes in g->block_size
 // Fast-path launch of a ragged batch in size order (k_order_by_size); the
-// permutation lives in stream-ordered scratch, so the call stays capturable.
-// Returns -ENOSYS when the batch is uniform or ordering is switched off.
+// permutation lives in the launch's scratch (above), so the call stays
+// capturable.  Returns -ENOSYS when the batch is uniform or ordering is
+// switched off.
 template <class F>
 static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 {
     if (!g->block_sizes || g->order || !nkfs_tune_now().size_order || g->nstripes > ORDER_MAXP * 1024u)
         return -ENOSYS;  // (k_order_by_size: ORDER_MAXP stripes per thread)
-    u32 *perm = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void **>(&perm), size_t(g->nstripes) * sizeof(u32), st) != hipSuccess)
+    Scratch sc;
+    u32 *perm = static_cast<u32 *>(sc.take(g, u64(g->nstripes) * sizeof(u32), st));
+    if (!perm)
         return -ENOSYS;
     hipLaunchKernelGGL(k_order_by_size, dim3(1), dim3(1024), 0, st, g->block_sizes, g->nstripes, g->k, perm);
     int rc = launch_ok();
     nkfs_geom g2 = *g;
     g2.order = perm;
+    sc.rest(&g2);
     if (!rc)
         rc = launch(&g2);
-    const hipError_t e = hipFreeAsync(perm, st);
-    return rc ? rc : (e == hipSuccess ? 0 : -EIO);
+    const int e = sc.finish();
+    return rc ? rc : e;
 }
 
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,

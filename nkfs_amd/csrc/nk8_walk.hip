@@ -39,6 +39,7 @@
 #include "gf256.h"
 #include "nk8_dev.h"
 #include "nkfs_internal.h"
+#include "scratch.h"
 #include "xxh64_dev.h"
 
 using namespace nkfs;
@@ -187,10 +188,37 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
     u8 *par0;
     if constexpr (RAGGED) {
         s0 = g.order ? g.order[blockIdx.x] : blockIdx.x;
+#ifdef NKFS_DEBUG_BOUNDS
+        // debug-bounds build (make DEBUG_BOUNDS=1): report and skip a stripe
+        // whose accesses would leave the caller's buffers
+        if (s0 >= g.nstripes) {
+            if (li == 0)
+                printf("nkfs bounds: k_encode_walk wave %u: order gives stripe %u of %u\n", blockIdx.x, s0,
+                       g.nstripes);
+            return;
+        }
+#endif
         B = g.block_sizes[s0];
         ppitch = (u64(part_size_of(B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
         blk0 = g.blocks + g.block_off[s0];
         par0 = g.parts + g.part_off[s0];
+#ifdef NKFS_DEBUG_BOUNDS
+        {
+            const u64 bo = g.block_off[s0], po = g.part_off[s0];
+            const bool bad = (g.blocks_bytes && bo + ((u64(B) + 3) & ~u64(3)) > g.blocks_bytes) ||
+                             (g.parts_bytes && po + u64(g.n) * ppitch > g.parts_bytes) || (po & 15) ||
+                             (g.block_size && B > g.block_size);
+            if (bad) {
+                if (li == 0)
+                    printf("nkfs bounds: k_encode_walk stripe %u: B %u block [%llu,+%u) of %llu, parts [%llu,+%llu) "
+                           "of %llu\n",
+                           s0, B, (unsigned long long)bo, B, (unsigned long long)g.blocks_bytes,
+                           (unsigned long long)po, (unsigned long long)(u64(g.n) * ppitch),
+                           (unsigned long long)g.parts_bytes);
+                return;
+            }
+        }
+#endif
     } else {
         s0 = blockIdx.x;
         B = g.block_size;
@@ -611,6 +639,16 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
         const u64 e = smap[w];
         slice = u32(e);
         s = g.order ? g.order[u32(e >> 32)] : u32(e >> 32);
+#ifdef NKFS_DEBUG_BOUNDS
+        if (s >= g.nstripes || u32(e >> 32) >= g.nstripes ||
+            (g.blocks_bytes && g.block_off[s] + g.block_sizes[s] > g.blocks_bytes) ||
+            (g.parts_bytes && g.part_off[s] + u64(n_slots) * ((u64(part_size_of(g.block_sizes[s], K)) + 255) & ~u64(255)) >
+                                  g.parts_bytes)) {
+            if (li == 0)
+                printf("nkfs bounds: k_decode_slice map entry %u -> stripe %u slice %u out of range\n", w, s, slice);
+            continue;
+        }
+#endif
     } else {
         s = w / slices;
         slice = w % slices;
@@ -978,14 +1016,17 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
     while (!g->block_sizes && units > 1 && u32(units / 2) * 1024u >= ps)
         units /= 2;
     const u32 slices = (ps + 1024u * units - 1) / (1024u * units);
-    // ragged: slice list in stream-ordered scratch -- nstripes + 2 u32 of
-    // prefix and total, then at most nstripes * slices(max) u64 map entries
+    // ragged: slice list in the launch's scratch (scratch.h) -- nstripes + 2
+    // u32 of prefix and total, then at most nstripes * slices(max) u64 map
+    // entries
     u32 *scan = nullptr;
     u64 *smap = nullptr;
+    Scratch sc;
     if (g->block_sizes) {
         const size_t head = ((size_t(g->nstripes) + 2) * sizeof(u32) + 15) & ~size_t(15);
-        if (hipMallocAsync(reinterpret_cast<void **>(&scan), head + size_t(g->nstripes) * slices * sizeof(u64), st) !=
-            hipSuccess)
+        // the caller's scratch is sized for 1,024-row units: any units fit
+        scan = static_cast<u32 *>(sc.take(g, head + size_t(g->nstripes) * slices * sizeof(u64), st, true));
+        if (!scan)
             return -ENOSYS;
         smap = reinterpret_cast<u64 *>(reinterpret_cast<u8 *>(scan) + head);
         hipLaunchKernelGGL(k_slice_scan, dim3(1), dim3(1024), 0, st, g->block_sizes, g->order, g->nstripes, g->k,
@@ -1012,8 +1053,9 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
     default:
         rc = -ENOSYS;
     }
-    if (scan && hipFreeAsync(scan, st) != hipSuccess && !rc)
-        rc = -EIO;
+    const int e = sc.finish();
+    if (!rc)
+        rc = e;
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "nk8_dev.h"
+#include "nkfs_internal.h"
 #include "xxh64_dev.h"
 
 using namespace nkfs;
@@ -33,7 +34,7 @@ using namespace nkfs::dev;
 
 // SB: single-buffered exchange (the hash wave copies its words to registers
 // between two barriers per chunk) -- half the LDS, so more workgroups per CU
-template <int K, int E, int NE, bool SB>
+template <int K, int E, int NE, bool SB, int PF>
 __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
     constexpr int S = 16 / E;       // stripes per workgroup: 4 accumulators x E parts x S = 64 chains
@@ -76,35 +77,42 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
             v = stripe_at(g, s);
         const bool aligned =
             ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
-        u32 d[4 * K];
-        auto load_task = [&](u32 r0) {
+        // PF register sets of chunk loads rotate: chunk c encodes from set
+        // c % PF and, once encoded, that set takes the loads of chunk c + PF,
+        // so with PF = 2 the next chunk's loads are in flight through this
+        // chunk's lookups as well as its stores (PF = 1: only its stores)
+        u32 d[PF][4 * K];
+        auto load_task = [&](u32 (&x)[4 * K], u32 r0) {
             const u64 off = u64(r0) * K;
             if (aligned && off + 16 * K <= v.B) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(v.blk + off);
 #pragma unroll
                 for (int q = 0; q < K; ++q) {
                     const uint4 t = src[q];
-                    d[4 * q] = t.x;
-                    d[4 * q + 1] = t.y;
-                    d[4 * q + 2] = t.z;
-                    d[4 * q + 3] = t.w;
+                    x[4 * q] = t.x;
+                    x[4 * q + 1] = t.y;
+                    x[4 * q + 2] = t.z;
+                    x[4 * q + 3] = t.w;
                 }
             } else {
 #pragma unroll
                 for (int q = 0; q < 4 * K; ++q) {
-                    u32 x = 0;
+                    u32 y = 0;
                     for (int b = 0; b < 4; ++b) {
                         const u64 p = off + 4 * q + b;
                         if (p < v.B)
-                            x |= u32(v.blk[p]) << (8 * b);
+                            y |= u32(v.blk[p]) << (8 * b);
                     }
-                    d[q] = x;
+                    x[q] = y;
                 }
             }
         };
         const u32 rbase = sub * 1024 + 16 * lane;  // this lane's first row in every chunk
-        if (live && rbase < v.ps)
-            load_task(rbase);  // first chunk requested before the table build
+        // first chunks requested before the table build
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (live && rbase + u32(p) * CR < v.ps)
+                load_task(d[p], rbase + u32(p) * CR);
 
         // tables of stripe gs, split over its WPS encoder waves
         u32 coef[W], idw[W];
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
         }
         __syncthreads();
 
-        for (u32 c = 0; c < nch; ++c) {
+        auto chunk = [&](u32 (&x)[4 * K], u32 c) {
             const u32 r0 = c * CR + rbase;
             if (live && r0 < v.ps) {
                 // 16 rows in four groups of 4: lookups + XOR, then the group's
@@ -145,14 +153,14 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
                         const int p0 = (4 * q + rr) * K;
-                        const u32 rep = __builtin_amdgcn_perm(0u, d[p0 >> 2], 0x01010101u * u32(p0 & 3));
+                        const u32 rep = __builtin_amdgcn_perm(0u, x[p0 >> 2], 0x01010101u * u32(p0 & 3));
 #pragma unroll
                         for (int w = 0; w < W; ++w)
                             row[rr][w] = rep;
 #pragma unroll
                         for (int m = 1; m < K; ++m) {
                             const int p = p0 + m;
-                            const u32 byte = (d[p >> 2] >> (8 * (p & 3))) & 0xFFu;
+                            const u32 byte = (x[p >> 2] >> (8 * (p & 3))) & 0xFFu;
                             const u8 *e = mytbl + tdep + (m - 1) * TB + byte * E;
                             if constexpr (E == 8) {
                                 const uint2 t = *reinterpret_cast<const uint2 *>(e);
@@ -173,8 +181,8 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
                     if constexpr (K * W > 8)
                         asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(out[0][q]));
                 }
-                if (r0 + CR < v.ps)
-                    load_task(r0 + CR);  // next chunk's rows in flight under this chunk's stores
+                if (r0 + PF * CR < v.ps)
+                    load_task(x, r0 + PF * CR);  // chunk c + PF's rows, in flight under what follows
                 u8 *xb = xbuf[SB ? 0 : (c & 1)] + gs * E * SP + sub * 1024 + 16 * lane;
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
@@ -193,6 +201,12 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
             __syncthreads();
             if constexpr (SB)
                 __syncthreads();  // the hash wave has copied the chunk
+        };
+        for (u32 c = 0; c < nch; c += PF) {
+            chunk(d[0], c);
+            if constexpr (PF == 2)
+                if (c + 1 < nch)
+                    chunk(d[PF - 1], c + 1);
         }
         return;
     }
@@ -281,7 +295,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     }
 }
 
-template <int E, int NE, bool SB>
+template <int E, int NE, bool SB, int PF>
 static int launch_ws(int k, hipStream_t st, const nkfs_geom &g, const uint8_t *ids, uint64_t *dig, bool nt)
 {
     constexpr int S = 16 / E;
@@ -289,7 +303,7 @@ static int launch_ws(int k, hipStream_t st, const nkfs_geom &g, const uint8_t *i
     switch (k) {
 #define NKFS_K(KK)                                                                         \
     case KK:                                                                               \
-        hipLaunchKernelGGL((k_encode_ws<KK, E, NE, SB>), grid, block, 0, st, g, ids, dig, nt); \
+        hipLaunchKernelGGL((k_encode_ws<KK, E, NE, SB, PF>), grid, block, 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -313,12 +327,17 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
     if (g->n > 8 || g->k > 8 || !digests)
         return -ENOSYS;
     int rc;
+    // chunks of loads in flight per encoder wave (struct nkfs_tune.enc_ws_prefetch)
+    const int pf = nkfs_tune_now().enc_ws_prefetch;
     if (g->n <= 4)
-        rc = ne == 8 ? launch_ws<4, 8, false>(g->k, st, *g, ids, digests, nt)
-                     : launch_ws<4, 4, false>(g->k, st, *g, ids, digests, nt);
+        rc = ne == 8 ? launch_ws<4, 8, false, 1>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<4, 4, false, 1>(g->k, st, *g, ids, digests, nt);
+    else if (pf >= 2)
+        rc = ne == 4 ? launch_ws<8, 4, false, 2>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<8, 2, false, 2>(g->k, st, *g, ids, digests, nt);
     else
-        rc = ne == 4 ? launch_ws<8, 4, false>(g->k, st, *g, ids, digests, nt)
-                     : launch_ws<8, 2, false>(g->k, st, *g, ids, digests, nt);
+        rc = ne == 4 ? launch_ws<8, 4, false, 1>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<8, 2, false, 1>(g->k, st, *g, ids, digests, nt);
     if (rc)
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -36,7 +36,23 @@ struct nkfs_geom {
 	 * batch between two kernels. */
 	uint32_t part_min;
 	uint32_t part_max;
+	/* optional device scratch for a launch's own metadata (the ragged
+	 * size order, the ragged slice map): the host pipeline carves it from
+	 * its context buffer; NULL = stream-ordered scratch from the library's
+	 * private memory pool (nkfs_scratch_alloc). */
+	uint8_t *scratch;
+	uint64_t scratch_bytes;
+	/* optional bounds of the caller's block / part buffers (bytes from
+	 * `blocks` / `parts`), checked by the debug-bounds build's device
+	 * asserts (make DEBUG_BOUNDS=1); 0 = unknown. */
+	uint64_t blocks_bytes;
+	uint64_t parts_bytes;
 };
+
+/* Scratch bytes the launchers take from nkfs_geom.scratch for a ragged
+ * batch of `nstripes` stripes whose parts span `sum_units` 1,024-row units
+ * in all (sum over stripes of ceil(part_size / 1024)). */
+uint64_t nkfs_ragged_scratch_bytes(uint32_t nstripes, uint64_t sum_units);
 
 /* Kernel choice and launch shape (struct nkfs_tune, include/nkfs_gpu.h):
  * one process-wide copy, set at init, read by the launchers. */

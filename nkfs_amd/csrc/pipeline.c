@@ -45,76 +45,78 @@ struct pin_ent {
 	uintptr_t base;
 	size_t bytes;
 	int refs;
+	int urefs; /* references held by nkfs_host_register (the rest: in-flight calls) */
 	struct pin_ent *next;
 };
 static pthread_mutex_t g_pin_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_pin_cv = PTHREAD_COND_INITIALIZER;
 static struct pin_ent *g_pins;
 
-/* Pin [p, p+bytes) for a call: memory the runtime already knows as pinned
- * (hipHostMalloc, torch pinned memory, a range someone else registered)
- * needs nothing; a range inside one this registry holds takes a reference;
- * a range that overlaps this registry's entries without lying inside one of
- * them is refused (-EBUSY: the entry's owner could unpin it mid-copy, and
- * the runtime would report the range as pinned); anything else is
- * registered here with one reference.  *held = the entry to release (NULL
- * when nothing was taken). */
-static int pin_take(const void *p, size_t bytes, struct pin_ent **held)
+/* Does the runtime know [p, p+bytes) as pinned host memory in one piece?
+ * The start pointer's attributes alone are not enough: a range that starts
+ * inside a pinned allocation and runs past its end would be DMA'd partly
+ * from pageable memory (round-3 fault audit). */
+static int runtime_pinned(const void *p, size_t bytes)
 {
-	*held = NULL;
-	if (!p || !bytes)
-		return 0;
-	const uintptr_t a = (uintptr_t)p;
-	int rc = 0;
-	pthread_mutex_lock(&g_pin_lock);
-	struct pin_ent *inside = NULL;
-	int overlaps = 0;
-	for (struct pin_ent *e = g_pins; e; e = e->next) {
-		if (a >= e->base && a + bytes <= e->base + e->bytes) {
-			inside = e;
-			break;
-		}
-		if (a < e->base + e->bytes && e->base < a + bytes)
-			overlaps = 1;
-	}
-	if (inside) {
-		inside->refs++;
-		*held = inside;
-		goto out;
-	}
-	if (overlaps) {
-		rc = -EBUSY;
-		goto out;
-	}
 	hipPointerAttribute_t attr;
-	if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) {
-		/* pinned by its owner; a range that only starts inside such an
-		 * allocation is the caller's contract (it must stay pinned) */
-		goto out;
+	if (hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeHost) {
+		(void)hipGetLastError();
+		return 0;
 	}
-	(void)hipGetLastError();
+	void *base = NULL;
+	size_t size = 0;
+	const void *dp = attr.devicePointer ? attr.devicePointer : p;
+	if (hipMemGetAddressRange(&base, &size, (void *)dp) != hipSuccess || !base || !size) {
+		(void)hipGetLastError();
+		return 1; /* no extent known: the start pointer's word (caller contract) */
+	}
+	/* the range's offset inside the allocation, in the allocation's own VA */
+	const uintptr_t off = (uintptr_t)dp - (uintptr_t)base;
+	return off + bytes >= off && off + bytes <= size;
+}
+
+/* Which of the registry's entries does [a, a+bytes) conflict with?  Returns
+ * the entry it lies inside (NULL if none) and sets *busy_user / *busy_call
+ * when it partly overlaps an entry registered by nkfs_host_register / by
+ * another in-flight call.  Caller holds g_pin_lock. */
+static struct pin_ent *pin_find(uintptr_t a, size_t bytes, int *busy_user, int *busy_call)
+{
+	*busy_user = *busy_call = 0;
+	for (struct pin_ent *e = g_pins; e; e = e->next) {
+		if (a >= e->base && a + bytes <= e->base + e->bytes)
+			return e;
+		if (a < e->base + e->bytes && e->base < a + bytes) {
+			if (e->urefs)
+				*busy_user = 1;
+			else
+				*busy_call = 1;
+		}
+	}
+	return NULL;
+}
+
+/* Register [a, a+bytes) as a new entry (caller holds g_pin_lock). */
+static int pin_new(uintptr_t a, size_t bytes, int user, struct pin_ent **held)
+{
 	struct pin_ent *e = malloc(sizeof(*e));
-	if (!e) {
-		rc = -ENOMEM;
-		goto out;
-	}
-	hipError_t he = hipHostRegister((void *)p, bytes, hipHostRegisterPortable);
+	if (!e)
+		return -ENOMEM;
+	hipError_t he = hipHostRegister((void *)a, bytes, hipHostRegisterPortable);
 	if (he != hipSuccess) {
 		(void)hipGetLastError();
 		free(e);
-		/* partly overlapping someone else's registration: refuse rather
-		 * than DMA from memory that may be unpinned mid-copy */
-		rc = he == hipErrorHostMemoryAlreadyRegistered ? -EBUSY : nkfs_hip_fail("hipHostRegister", (int)he);
-		goto out;
+		/* partly overlapping a registration made outside this registry:
+		 * refuse rather than DMA from memory that may be unpinned mid-copy */
+		return he == hipErrorHostMemoryAlreadyRegistered ? -EBUSY : nkfs_hip_fail("hipHostRegister", (int)he);
 	}
 	e->base = a;
 	e->bytes = bytes;
 	e->refs = 1;
+	e->urefs = user;
 	e->next = g_pins;
 	g_pins = e;
 	*held = e;
-out:
-	pthread_mutex_unlock(&g_pin_lock);
-	return rc;
+	return 0;
 }
 
 /* caller holds g_pin_lock */
@@ -126,8 +128,15 @@ static void pin_drop_locked(struct pin_ent *e)
 				*pp = e->next;
 				break;
 			}
-		hipHostUnregister((void *)e->base);
+		const hipError_t he = hipHostUnregister((void *)e->base);
+		if (he != hipSuccess) {
+			/* the runtime still holds it: say so (a later call on a reused
+			 * mapping would otherwise be trusted as pinned) */
+			(void)hipGetLastError();
+			nkfs_hip_fail("hipHostUnregister", (int)he);
+		}
 		free(e);
+		pthread_cond_broadcast(&g_pin_cv);
 	}
 }
 
@@ -140,14 +149,97 @@ static void pin_drop(struct pin_ent *e)
 	pthread_mutex_unlock(&g_pin_lock);
 }
 
+/* Pin the ranges a host call DMAs from / to ([p[i], p[i]+bytes[i]), i < 2;
+ * NULL or empty ranges are skipped) for the duration of the call, in one
+ * step under the registry lock:
+ *  - memory the runtime already knows as pinned over the whole range
+ *    (hipHostMalloc, torch pinned memory) needs nothing;
+ *  - a range inside an entry of this registry takes a reference;
+ *  - a range that partly overlaps an nkfs_host_register entry is refused
+ *    (-EBUSY: the entry's owner could unpin it mid-copy);
+ *  - a range that partly overlaps another call's temporary entry waits until
+ *    that call drops it (nothing is held while waiting, so two calls cannot
+ *    wait on each other);
+ *  - anything else is registered here for the call.
+ * Two ranges of one call that overlap each other are pinned as their union.
+ * held[i] = the entry to release (NULL when nothing was taken). */
+static int pin_take2(const void *const p[2], const size_t bytes[2], struct pin_ent *held[2])
+{
+	uintptr_t a[2] = { (uintptr_t)p[0], (uintptr_t)p[1] };
+	size_t nb[2] = { p[0] ? bytes[0] : 0, p[1] ? bytes[1] : 0 };
+	held[0] = held[1] = NULL;
+	int share = 0; /* range 1 rides on range 0's entry */
+	if (nb[0] && nb[1] && a[0] < a[1] + nb[1] && a[1] < a[0] + nb[0]) {
+		const uintptr_t lo = a[0] < a[1] ? a[0] : a[1];
+		const uintptr_t hi = a[0] + nb[0] > a[1] + nb[1] ? a[0] + nb[0] : a[1] + nb[1];
+		a[0] = lo;
+		nb[0] = hi - lo;
+		nb[1] = 0;
+		share = 1;
+	}
+	int rc = 0;
+	pthread_mutex_lock(&g_pin_lock);
+	/* the registry first (a range inside an in-flight call's entry must take
+	 * a reference: the runtime would also call it pinned, until that call
+	 * unpins it), then the runtime's own pinned allocations */
+	for (;;) {
+		int wait = 0;
+		for (int i = 0; i < 2 && !rc; i++) {
+			int bu, bc;
+			if (!nb[i] || pin_find(a[i], nb[i], &bu, &bc))
+				continue;
+			if (bu)
+				rc = -EBUSY;
+			else if (bc)
+				wait = 1;
+		}
+		if (rc || !wait)
+			break;
+		pthread_cond_wait(&g_pin_cv, &g_pin_lock);
+	}
+	for (int i = 0; i < 2 && !rc; i++) {
+		if (!nb[i])
+			continue;
+		int bu, bc;
+		struct pin_ent *in = pin_find(a[i], nb[i], &bu, &bc);
+		if (in) {
+			in->refs++;
+			held[i] = in;
+		} else if (!runtime_pinned((const void *)a[i], nb[i])) {
+			rc = pin_new(a[i], nb[i], 0, &held[i]);
+		}
+	}
+	if (rc)
+		for (int i = 0; i < 2; i++)
+			if (held[i]) {
+				pin_drop_locked(held[i]);
+				held[i] = NULL;
+			}
+	pthread_mutex_unlock(&g_pin_lock);
+	(void)share;
+	return rc;
+}
+
 int nkfs_host_register(void *p, size_t bytes)
 {
-	struct pin_ent *e;
 	if (!p || !bytes)
 		return -EINVAL;
-	int rc = pin_take(p, bytes, &e);
-	if (!rc && !e)
-		return -EEXIST; /* pinned by its owner: nothing to hold */
+	const uintptr_t a = (uintptr_t)p;
+	int rc = 0;
+	pthread_mutex_lock(&g_pin_lock);
+	int bu, bc;
+	struct pin_ent *in = pin_find(a, bytes, &bu, &bc), *e = NULL;
+	if (in) {
+		in->refs++;
+		in->urefs++; /* now also the caller's registration */
+	} else if (bu || bc) {
+		rc = -EBUSY;
+	} else if (runtime_pinned(p, bytes)) {
+		rc = -EEXIST; /* pinned by its owner: nothing to hold */
+	} else {
+		rc = pin_new(a, bytes, 1, &e);
+	}
+	pthread_mutex_unlock(&g_pin_lock);
 	return rc;
 }
 
@@ -157,10 +249,12 @@ int nkfs_host_unregister(void *p)
 	 * free the entry in between */
 	pthread_mutex_lock(&g_pin_lock);
 	struct pin_ent *e = g_pins;
-	while (e && e->base != (uintptr_t)p)
+	while (e && !(e->base == (uintptr_t)p && e->urefs))
 		e = e->next;
-	if (e)
+	if (e) {
+		e->urefs--;
 		pin_drop_locked(e);
+	}
 	pthread_mutex_unlock(&g_pin_lock);
 	return e ? 0 : -ENOENT;
 }
@@ -226,7 +320,7 @@ static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
 /* Device / pinned scratch layout of one sub-batch of at most `cnt` stripes
  * (offsets into the context buffers). */
 struct lay {
-	uint64_t d_blk, d_parts, d_boff, d_poff, d_sz, d_ids, d_avail, d_dig, d_status, d_bad, d_work, d_total;
+	uint64_t d_blk, d_parts, d_boff, d_poff, d_sz, d_ids, d_avail, d_dig, d_status, d_bad, d_work, d_scr, d_total;
 	uint64_t h_boff, h_poff, h_sz, h_ids, h_avail, h_dig, h_status, h_bad, h_stage, h_total;
 };
 
@@ -272,6 +366,9 @@ static void sub_ranges(const struct hp *h, struct sub *u)
 
 static int hp_paged(const struct hp *h) { return h->pages != NULL; }
 
+static int ragged_ok(const uint32_t *sizes, const uint64_t *boff, const uint64_t *poff, uint32_t nstripes,
+		     uint32_t max_block, int nsl, int k);
+
 /* device bytes of the blocks of [s0, s1) */
 static uint64_t dev_block_bytes(const struct hp *h, const struct sub *u)
 {
@@ -283,7 +380,8 @@ static uint64_t dev_block_bytes(const struct hp *h, const struct sub *u)
 	return t;
 }
 
-static void layout(const struct hp *h, uint32_t cnt, uint64_t blk_bytes, uint64_t part_bytes, struct lay *L)
+static void layout(const struct hp *h, uint32_t cnt, uint64_t blk_bytes, uint64_t part_bytes, uint64_t scr_bytes,
+		   struct lay *L)
 {
 	const uint64_t nsl = (uint64_t)hp_slots(h);
 	uint64_t o = 0;
@@ -309,6 +407,8 @@ static void layout(const struct hp *h, uint32_t cnt, uint64_t blk_bytes, uint64_
 	o += align256(cnt * 8ull);
 	L->d_work = o;
 	o += align256(nkfs_decode_work_bytes(cnt, h->k));
+	L->d_scr = o;
+	o += align256(scr_bytes);
 	L->d_total = o;
 
 	o = 0;
@@ -427,6 +527,60 @@ static void pages_copy(const struct hp *h, uint32_t s0, uint32_t s1, uint8_t *bu
 	free(off);
 }
 
+/* Sub-batch u's metadata into the pinned scratch `hb` (layout L): ids
+ * (+ survivor lists and expected digests for a verifying decode) and, for
+ * ragged batches, the block / part offsets shifted so that they land in
+ * this context's device buffers, and the sizes.  [*lo, *hi) = the host range
+ * the one metadata H2D copies (its device image starts at d_boff + (*lo -
+ * h_boff): the two layouts list these regions in the same order). */
+static void fill_meta(const struct hp *h, const struct sub *u, const struct lay *L, uint8_t *hb, uint64_t *lo,
+		      uint64_t *hi)
+{
+	const uint32_t cnt = u->s1 - u->s0;
+	const int nsl = hp_slots(h);
+	memcpy(hb + L->h_ids, h->ids + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl);
+	uint64_t meta_lo = L->h_ids, meta_hi = L->h_ids + (uint64_t)cnt * nsl;
+	if (h->dir == HP_DEC) {
+		memcpy(hb + L->h_avail, h->avail + (uint64_t)u->s0 * h->navail, (size_t)cnt * h->navail);
+		meta_hi = L->h_avail + (uint64_t)cnt * h->navail;
+		if (h->expect) {
+			memcpy(hb + L->h_dig, h->expect + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl * 8);
+			meta_hi = L->h_dig + (uint64_t)cnt * nsl * 8;
+		}
+	}
+	if (h->sizes) {
+		uint64_t *bo = (uint64_t *)(hb + L->h_boff), *po = (uint64_t *)(hb + L->h_poff);
+		uint32_t *sz = (uint32_t *)(hb + L->h_sz);
+		uint64_t packed = 0;
+		for (uint32_t s = u->s0; s < u->s1; s++) {
+			const uint32_t B = hp_B(h, s);
+			if (hp_paged(h)) {
+				bo[s - u->s0] = packed;
+				packed += align256(B);
+			} else {
+				bo[s - u->s0] = h->boff[s] - u->blo;
+			}
+			po[s - u->s0] = h->poff[s] - u->plo;
+			sz[s - u->s0] = B;
+		}
+		meta_lo = L->h_boff;
+	}
+	*lo = meta_lo;
+	*hi = meta_hi;
+}
+
+/* Device scratch the launchers take for sub-batch u (ragged: size order +
+ * slice map, nkfs_ragged_scratch_bytes; uniform batches need none). */
+static uint64_t sub_scratch(const struct hp *h, const struct sub *u)
+{
+	if (!h->sizes)
+		return 0;
+	uint64_t units = 0;
+	for (uint32_t s = u->s0; s < u->s1; s++)
+		units += ((uint64_t)nkfs_part_size(hp_B(h, s), h->k) + 1023) / 1024;
+	return nkfs_ragged_scratch_bytes(u->s1 - u->s0, units);
+}
+
 #define HIPGO(call, what)                                              \
 	do {                                                           \
 		hipError_t e_ = (call);                                \
@@ -457,33 +611,8 @@ static int issue(const struct hp *h, struct ctxs *x)
 	const int paged = hp_paged(h);
 
 	/* metadata into pinned scratch: ids (+ survivor lists), ragged offsets */
-	memcpy(hb + L->h_ids, h->ids + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl);
-	uint64_t meta_lo = L->h_ids, meta_hi = L->h_ids + (uint64_t)cnt * nsl;
-	if (h->dir == HP_DEC) {
-		memcpy(hb + L->h_avail, h->avail + (uint64_t)u->s0 * h->navail, (size_t)cnt * h->navail);
-		meta_hi = L->h_avail + (uint64_t)cnt * h->navail;
-		if (h->expect) {
-			memcpy(hb + L->h_dig, h->expect + (uint64_t)u->s0 * nsl, (size_t)cnt * nsl * 8);
-			meta_hi = L->h_dig + (uint64_t)cnt * nsl * 8;
-		}
-	}
-	if (h->sizes) {
-		uint64_t *bo = (uint64_t *)(hb + L->h_boff), *po = (uint64_t *)(hb + L->h_poff);
-		uint32_t *sz = (uint32_t *)(hb + L->h_sz);
-		uint64_t packed = 0;
-		for (uint32_t s = u->s0; s < u->s1; s++) {
-			const uint32_t B = hp_B(h, s);
-			if (paged) {
-				bo[s - u->s0] = packed;
-				packed += align256(B);
-			} else {
-				bo[s - u->s0] = h->boff[s] - u->blo;
-			}
-			po[s - u->s0] = h->poff[s] - u->plo;
-			sz[s - u->s0] = B;
-		}
-		meta_lo = L->h_boff;
-	}
+	uint64_t meta_lo, meta_hi;
+	fill_meta(h, u, L, hb, &meta_lo, &meta_hi);
 	HIPGO(hipMemcpyAsync(d + L->d_boff + (meta_lo - L->h_boff), hb + meta_lo, meta_hi - meta_lo,
 			     hipMemcpyHostToDevice, st),
 	      "H2D (metadata)");
@@ -517,6 +646,12 @@ static int issue(const struct hp *h, struct ctxs *x)
 	g.nstripes = cnt;
 	g.blocks = d + L->d_blk;
 	g.parts = d + L->d_parts;
+	g.blocks_bytes = L->d_parts - L->d_blk;
+	g.parts_bytes = L->d_boff - L->d_parts;
+	if (L->d_total > L->d_scr) {
+		g.scratch = d + L->d_scr;
+		g.scratch_bytes = L->d_total - L->d_scr;
+	}
 	if (h->sizes) {
 		g.block_size = h->max_block;
 		g.block_off = (const uint64_t *)(d + L->d_boff);
@@ -659,15 +794,16 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 	if (s0 >= s1)
 		return 0;
 	/* scratch sized for the largest sub-batch of this lane */
-	uint64_t max_blk = 0, max_parts = 0;
+	uint64_t max_blk = 0, max_parts = 0, max_scr = 0;
 	uint32_t max_cnt = 0;
 	for (uint32_t s = s0; s < s1;) {
 		struct sub u = { .s0 = s, .s1 = sub_end(h, s, s1) };
 		sub_ranges(h, &u);
-		const uint64_t bb = dev_block_bytes(h, &u);
+		const uint64_t bb = dev_block_bytes(h, &u), sb = sub_scratch(h, &u);
 		max_blk = bb > max_blk ? bb : max_blk;
 		max_parts = u.phi - u.plo > max_parts ? u.phi - u.plo : max_parts;
 		max_cnt = u.s1 - u.s0 > max_cnt ? u.s1 - u.s0 : max_cnt;
+		max_scr = sb > max_scr ? sb : max_scr;
 		s = u.s1;
 	}
 	struct ctxs xs[NSTREAM];
@@ -675,7 +811,7 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 	int rc = 0;
 	for (int i = 0; i < NSTREAM; i++) {
 		struct ctxs *x = &xs[i];
-		layout(h, max_cnt, max_blk, max_parts, &x->L);
+		layout(h, max_cnt, max_blk, max_parts, max_scr, &x->L);
 		void *dv, *hv;
 		if (!(x->c = nkfs_ctx_get_on(dev))) {
 			rc = -ENOMEM;
@@ -764,14 +900,12 @@ static int hp_run(struct hp *h)
 		total += hp_B(h, s);
 	}
 	(void)nsl;
-	struct pin_ent *pb = NULL, *pp = NULL;
-	int rc = 0;
-	if (!hp_paged(h) && (rc = pin_take(h->blocks, bend, &pb)))
+	struct pin_ent *held[2];
+	const void *rp[2] = { hp_paged(h) ? NULL : h->blocks, h->parts };
+	const size_t rb[2] = { bend, pend };
+	int rc = pin_take2(rp, rb, held);
+	if (rc)
 		return rc;
-	if ((rc = pin_take(h->parts, pend, &pp))) {
-		pin_drop(pb);
-		return rc;
-	}
 	int lanes[NKFS_MAX_DEVICES];
 	int nl = nkfs_gpu_get_devices(lanes, NKFS_MAX_DEVICES);
 	if (nl > (int)h->nstripes)
@@ -810,8 +944,137 @@ static int hp_run(struct hp *h)
 			rc = L[i].rc;
 		nkfs_use_device(nkfs_gpu_device());
 	}
-	pin_drop(pp);
-	pin_drop(pb);
+	pin_drop(held[1]);
+	pin_drop(held[0]);
+	return rc;
+}
+
+/* ------------------------------------------------------------ plan check */
+
+#define CHK(cond, ...)                                                         \
+	do {                                                                   \
+		if (!(cond)) {                                                 \
+			if (msg && msg_len)                                    \
+				snprintf(msg, msg_len, __VA_ARGS__);           \
+			rc = -ERANGE;                                          \
+			goto out;                                              \
+		}                                                              \
+	} while (0)
+
+static int in_range(uint64_t lo, uint64_t len, uint64_t rlo, uint64_t rhi)
+{
+	return lo >= rlo && lo + len >= lo && lo + len <= rhi;
+}
+
+/* CPU replay of a ragged host call's plan (hp_run -> run_lane -> issue):
+ * the same sub-batch cuts, layout and shifted offsets (fill_meta writes
+ * them into a host copy of the pinned scratch), then every access the
+ * kernels and copies of each sub-batch make is checked against the region
+ * it must stay in: block reads up to the walk encoder's dword-rounded
+ * num_records, part stores over the stripe's n_slots * pitch, the metadata
+ * image, the launchers' scratch, the caller-side copy ranges.  Touches no
+ * GPU (round-3 fault audit; tests/test_abi.py). */
+int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *block_size, uint32_t max_block_size,
+			uint32_t nstripes, int n_slots, int k, int navail, const uint64_t *part_off, uint32_t page_size,
+			uint64_t chunk_bytes, char *msg, size_t msg_len)
+{
+	if (!block_size || !part_off || (!page_size && !block_off) || nkfs_bad_params(max_block_size, n_slots, k) ||
+	    (decode && (navail < k || navail > n_slots)) ||
+	    !ragged_ok(block_size, page_size ? NULL : block_off, part_off, nstripes, max_block_size, n_slots, k))
+		return -EINVAL;
+	uint64_t *first = NULL;
+	uint8_t *ids = NULL, *avail = NULL, *hb = NULL;
+	int rc = 0, subs = 0;
+	first = calloc(nstripes ? nstripes : 1, sizeof(*first));
+	ids = calloc((size_t)(nstripes ? nstripes : 1) * n_slots, 1);
+	avail = calloc((size_t)(nstripes ? nstripes : 1) * (navail > 0 ? navail : 1), 1);
+	if (!first || !ids || !avail) {
+		rc = -ENOMEM;
+		goto out;
+	}
+	struct hp h = { .dir = decode ? HP_DEC : HP_ENC, .n = n_slots, .k = k, .n_slots = decode ? n_slots : 0,
+			.navail = decode ? navail : 0, .nstripes = nstripes, .max_block = max_block_size,
+			.sizes = block_size, .boff = page_size ? NULL : block_off, .poff = part_off, .ids = ids,
+			.avail = avail, .chunk = chunk_bytes ? chunk_bytes : 32ull << 20 };
+	if (page_size) { /* page lists: only the packed staging matters here */
+		h.pages = (uint8_t *const *)first; /* non-NULL marker, never dereferenced */
+		h.first_page = first;
+		h.page_size = page_size;
+	}
+	/* caller buffer extents (hp_run) */
+	uint64_t bend = 0, pend = 0;
+	for (uint32_t s = 0; s < nstripes; s++) {
+		const uint64_t be = hp_bofs(&h, s) + hp_B(&h, s), pe = hp_pofs(&h, s) + hp_pspan(&h, s);
+		bend = be > bend ? be : bend;
+		pend = pe > pend ? pe : pend;
+	}
+	/* run_lane's scratch sizing */
+	uint64_t max_blk = 0, max_parts = 0, max_scr = 0;
+	uint32_t max_cnt = 0;
+	for (uint32_t s = 0; s < nstripes;) {
+		struct sub u = { .s0 = s, .s1 = sub_end(&h, s, nstripes) };
+		sub_ranges(&h, &u);
+		const uint64_t bb = dev_block_bytes(&h, &u), sb = sub_scratch(&h, &u);
+		max_blk = bb > max_blk ? bb : max_blk;
+		max_parts = u.phi - u.plo > max_parts ? u.phi - u.plo : max_parts;
+		max_cnt = u.s1 - u.s0 > max_cnt ? u.s1 - u.s0 : max_cnt;
+		max_scr = sb > max_scr ? sb : max_scr;
+		s = u.s1;
+	}
+	struct lay L;
+	layout(&h, max_cnt, max_blk, max_parts, max_scr, &L);
+	CHK(L.d_blk < L.d_parts && L.d_parts <= L.d_boff && L.d_boff <= L.d_poff && L.d_poff <= L.d_sz &&
+		    L.d_sz <= L.d_ids && L.d_ids <= L.d_avail && L.d_avail <= L.d_dig && L.d_dig <= L.d_status &&
+		    L.d_status <= L.d_bad && L.d_bad <= L.d_work && L.d_work <= L.d_scr && L.d_scr <= L.d_total,
+	    "device layout regions out of order");
+	CHK(L.d_ids - L.d_boff == L.h_ids - L.h_boff && L.d_dig - L.d_boff == L.h_dig - L.h_boff,
+	    "host and device metadata images differ");
+	hb = calloc(L.h_total ? L.h_total : 1, 1);
+	if (!hb) {
+		rc = -ENOMEM;
+		goto out;
+	}
+	for (uint32_t s = 0; s < nstripes; subs++) {
+		struct sub u = { .s0 = s, .s1 = sub_end(&h, s, nstripes) };
+		sub_ranges(&h, &u);
+		const uint32_t cnt = u.s1 - u.s0;
+		uint64_t lo, hi;
+		fill_meta(&h, &u, &L, hb, &lo, &hi);
+		CHK(in_range(L.d_boff + (lo - L.h_boff), hi - lo, L.d_boff, L.d_status), "sub-batch %d: metadata image", subs);
+		if (!page_size) {
+			CHK(in_range(u.blo, u.bhi - u.blo, 0, bend), "sub-batch %d: block H2D/D2H range", subs);
+			CHK(u.bhi - u.blo <= L.d_parts - L.d_blk, "sub-batch %d: blocks exceed the device region", subs);
+		}
+		CHK(in_range(u.plo, u.phi - u.plo, 0, pend), "sub-batch %d: part copy range", subs);
+		CHK(u.phi - u.plo <= L.d_boff - L.d_parts, "sub-batch %d: parts exceed the device region", subs);
+		CHK(sub_scratch(&h, &u) <= L.d_total - L.d_scr, "sub-batch %d: launcher scratch", subs);
+		CHK((uint64_t)cnt * n_slots * 8 <= L.d_status - L.d_dig, "sub-batch %d: digest region", subs);
+		CHK(nkfs_decode_work_bytes(cnt, k) <= L.d_scr - L.d_work, "sub-batch %d: decode workspace", subs);
+		const uint64_t *bo = (const uint64_t *)(hb + L.h_boff), *po = (const uint64_t *)(hb + L.h_poff);
+		const uint32_t *sz = (const uint32_t *)(hb + L.h_sz);
+		for (uint32_t i = 0; i < cnt; i++) {
+			const uint32_t B = sz[i];
+			CHK(B == hp_B(&h, u.s0 + i), "stripe %u: size image", u.s0 + i);
+			/* block side: reads up to the dword-rounded num_records of the
+			 * walk encoder's buffer resource; decode writes [bo, bo + B) */
+			CHK(in_range(bo[i], ((uint64_t)B + 3) & ~3ull, 0, L.d_parts - L.d_blk),
+			    "stripe %u: block bytes [%llu, +%u) outside the device block region (%llu)", u.s0 + i,
+			    (unsigned long long)bo[i], B, (unsigned long long)(L.d_parts - L.d_blk));
+			CHK(in_range(po[i], (uint64_t)n_slots * nkfs_part_pitch(B, k), 0, L.d_boff - L.d_parts),
+			    "stripe %u: parts [%llu, +%llu) outside the device part region", u.s0 + i,
+			    (unsigned long long)po[i], (unsigned long long)((uint64_t)n_slots * nkfs_part_pitch(B, k)));
+			CHK((po[i] & 15) == 0, "stripe %u: part base not 16-byte aligned", u.s0 + i);
+		}
+		s = u.s1;
+	}
+	if (msg && msg_len)
+		snprintf(msg, msg_len, "ok: %d sub-batch(es), device %llu B per context", subs,
+			 (unsigned long long)L.d_total);
+out:
+	free(hb);
+	free(avail);
+	free(ids);
+	free(first);
 	return rc;
 }
 

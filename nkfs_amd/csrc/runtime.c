@@ -60,6 +60,7 @@ static struct nkfs_tune g_tune = {
 	.enc_fused_waves_per_cu = 0,
 	.dec_wave_waves_per_cu = 0,
 	.dec_run_units = 4,
+	.enc_ws_prefetch = 1,
 };
 
 void nkfs_tune_get(struct nkfs_tune *t)
@@ -82,7 +83,8 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->enc_fused_waves_per_cu && (t->enc_fused_waves_per_cu < 3 || t->enc_fused_waves_per_cu > 32)) ||
 	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)) ||
 	    (t->dec_run_units != 1 && t->dec_run_units != 2 && t->dec_run_units != 4 && t->dec_run_units != 8 &&
-	     t->dec_run_units != 16))
+	     t->dec_run_units != 16) ||
+	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;
@@ -356,6 +358,8 @@ struct nkfs_ctx *nkfs_ctx_get(void)
 	return ready_now() ? nkfs_ctx_get_on(g_device) : NULL;
 }
 
+#define POOL_KEEP 16
+
 void nkfs_ctx_put(struct nkfs_ctx *c)
 {
 	if (!c)
@@ -364,10 +368,27 @@ void nkfs_ctx_put(struct nkfs_ctx *c)
 		free(c);
 		return;
 	}
+	/* the idle pool keeps at most POOL_KEEP contexts per device: a burst
+	 * (many pending checksum states, many concurrent host calls) does not
+	 * hold its streams and pinned / device scratch for the process's life */
+	int n = 0;
 	pthread_mutex_lock(&g_lock);
-	c->next = g_dev[c->dev].pool;
-	g_dev[c->dev].pool = c;
+	for (struct nkfs_ctx *e = g_dev[c->dev].pool; e; e = e->next)
+		n++;
+	if (n < POOL_KEEP) {
+		c->next = g_dev[c->dev].pool;
+		g_dev[c->dev].pool = c;
+		c = NULL;
+	}
 	pthread_mutex_unlock(&g_lock);
+	if (c) {
+		int cur = -1;
+		(void)hipGetDevice(&cur);
+		nkfs_use_device(c->dev);
+		ctx_destroy(c);
+		if (cur >= 0)
+			nkfs_use_device(cur);
+	}
 }
 
 int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out)
@@ -446,7 +467,7 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
-			       nstripes, n, k, NULL, 0, 0 };
+			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
 	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
@@ -466,7 +487,7 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
-			       nstripes, n, k, NULL, 0, 0 };
+			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
 	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
@@ -493,7 +514,7 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
-			       nstripes, n_slots, k, NULL, 0, 0 };
+			       nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0 };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
 				  d_badmask);
 }
@@ -524,7 +545,7 @@ static int decode_ragged_common(const uint8_t *d_parts, const uint64_t *d_part_o
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, (uint8_t *)d_parts, 0,
-			       d_part_off, nstripes, n_slots, k, NULL, 0, 0 };
+			       d_part_off, nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0 };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
 				  d_badmask);
 }

@@ -118,3 +118,74 @@ def test_decode_workspace_covers_every_plan_layout():
             loc = (S * stride + 15) & ~15
             gsum = (loc + 4 * S + 15) & ~15
             assert w >= gsum + 4 * ((S + 255) // 256), (S, k)
+
+
+def _ragged(sizes, n_slots, k, block_gap, part_gap):
+    import numpy as np
+    L = _lib.lib()
+    boff = np.zeros(len(sizes), np.uint64)
+    poff = np.zeros(len(sizes), np.uint64)
+    pos = ppos = 0
+    for s, B in enumerate(sizes):
+        boff[s], poff[s] = pos, ppos
+        pos += int(B) + block_gap
+        ppos += n_slots * L.nkfs_part_pitch(int(B), k) + part_gap
+    return boff, poff
+
+
+def _plan(decode, boff, sizes, n, k, navail, poff, page, chunk):
+    import numpy as np
+    L = _lib.lib()
+    sz = np.ascontiguousarray(sizes, np.uint32)
+    msg = C.create_string_buffer(256)
+    rc = L.nkfs_pipeline_check(decode, None if boff is None else boff.ctypes.data, sz.ctypes.data, int(sz.max()),
+                               len(sz), n, k, navail, poff.ctypes.data, page, chunk, msg, 256)
+    return rc, msg.value.decode()
+
+
+def test_pipeline_plan_round3_fault_geometry():
+    """CPU replay of the host pipeline's plan (sub-batch cuts, device layout,
+    shifted ragged offsets: pipeline.c issue()) for the geometry of the
+    round-3 fault (test_ragged_host_gaps_untouched[8-5-0]: N8K5, 1 MiB + 1 B
+    + 70,001 B + mixed sizes, block gap 24, part gap 48): every kernel access
+    and copy of every sub-batch stays inside its region, for PUT and GET and
+    the three sub-batch sizes the GPU test uses."""
+    from nkfs_amd import synth
+    for n, k in ((8, 5), (4, 2), (6, 3)):
+        sizes = synth.mixed_sizes(29)
+        sizes[:3] = (1048576, 1, 70001)
+        boff, poff = _ragged(sizes, n, k, 24, 48)
+        for chunk in (0, 1 << 20, 100000, 1):
+            for dec in (0, 1):
+                rc, msg = _plan(dec, boff, sizes, n, k, n, poff, 0, chunk)
+                assert rc == 0, (n, k, chunk, dec, msg)
+                assert msg.startswith("ok")
+
+
+def test_pipeline_plan_random_geometries():
+    """The same replay over random ragged batches: sizes 1 B .. 2 MiB,
+    unaligned block gaps, 16-byte part gaps, page-list staging, sub-batch
+    sizes from one stripe to all of them."""
+    import numpy as np
+    rng = np.random.default_rng(4)
+    for trial in range(60):
+        n = int(rng.integers(2, 17))
+        k = int(rng.integers(2, n + 1))
+        S = int(rng.integers(1, 120))
+        sizes = np.where(rng.random(S) < 0.2, rng.integers(1, 64, S), rng.integers(1, 2 << 20, S)).astype(np.uint32)
+        boff, poff = _ragged(sizes, n, k, int(rng.integers(0, 97)), 16 * int(rng.integers(0, 9)))
+        chunk = int(rng.choice([0, 1, 4096, 1 << 20, 7 << 20]))
+        page = int(rng.choice([0, 0, 4096, 512]))
+        rc, msg = _plan(int(trial & 1), None if page else boff, sizes, n, k, n, poff, page, chunk)
+        assert rc == 0, (trial, msg)
+
+
+def test_pipeline_plan_rejects_bad_geometry():
+    import numpy as np
+    sizes = np.array([4096, 4096], np.uint32)
+    boff, poff = _ragged(sizes, 4, 2, 0, 0)
+    poff[1] += 8  # part bases must be 16-byte aligned
+    assert _plan(0, boff, sizes, 4, 2, 4, poff, 0, 0)[0] == -22
+    boff, poff = _ragged(sizes, 4, 2, 0, 0)
+    boff[1] -= 1  # blocks overlap
+    assert _plan(0, boff, sizes, 4, 2, 4, poff, 0, 0)[0] == -22

@@ -111,8 +111,8 @@ def test_reset_and_free_pending(L, O):
 
 
 def test_more_pending_states_than_slots(L, O):
-    """1,100 messages pending at once (1,024 slots): the rest fold
-    synchronously; every digest, taken in reverse order, is exact."""
+    """1,100 messages pending at once (64 slots, csum.c NSLOT): the rest
+    fold synchronously; every digest, taken in reverse order, is exact."""
     from nkfs_amd import crt
     rng = np.random.default_rng(8)
     datas = [rng.integers(0, 256, int(rng.integers(32, 3000)), dtype=np.uint8) for _ in range(1100)]
@@ -151,3 +151,45 @@ def test_threads(L, O):
     for t in th:
         t.join()
     assert got == want
+
+
+def test_poisoned_state_fails_until_reset(L, O):
+    """A failed update poisons the state (it would otherwise look
+    valid and digest to a wrong sum): every later update returns XXH_ERROR
+    until XXH64_reset, which clears it without touching any slot.  The poison
+    word (PEND_MAGIC | 0xFFFF in the 88-byte state's padding, offset 84) is
+    what csum.c writes on that path."""
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, 256, 5000, dtype=np.uint8)
+    st = _state(L)
+    _upd(L, st, a[:10])  # buffered on the host: no slot held
+    C.c_uint32.from_address(st + 84).value = 0xC5A1FFFF
+    assert L.XXH64_update(st, a.ctypes.data, a.size) == 1  # XXH_ERROR
+    assert L.XXH64_update(st, a.ctypes.data, a.size) == 1
+    assert L.XXH64_reset(st, 0) == 0
+    _upd(L, st, a)
+    assert L.XXH64_digest(st) == O.xxh64(a)
+    L.XXH64_freeState(st)
+
+
+def test_concurrent_digests_of_one_state(L, O):
+    """The reference's digest is read-only, so one state may be digested
+    from several threads at once; a pending message is completed once, under
+    its slot's lock, and every thread gets the same exact digest."""
+    rng = np.random.default_rng(13)
+    for trial in range(20):
+        a = rng.integers(0, 256, int(rng.integers(64, 400000)), dtype=np.uint8)
+        st = _state(L)
+        _upd(L, st, a)  # pending on the GPU
+        got = [None] * 4
+
+        def dig(i):
+            got[i] = L.XXH64_digest(st)
+
+        th = [threading.Thread(target=dig, args=(i,)) for i in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert got == [O.xxh64(a)] * 4, trial
+        L.XXH64_freeState(st)

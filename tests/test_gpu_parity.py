@@ -841,15 +841,15 @@ def test_bench_kernels_against_oracle(L, O, S, B):
     ids = dev(ids_np)
     ps = batch.part_size(B, k)
     sample = sorted({int(x) for x in np.linspace(0, S - 1, 16)})
-    for kern in ("ws", "walk"):
-        with _tuned(enc_kernel=_enc(kern)):
+    for kern, pf in (("ws", 1), ("ws", 2), ("walk", 1)):
+        with _tuned(enc_kernel=_enc(kern), enc_ws_prefetch=pf):
             parts, dig = batch.encode(blocks, B, n, k, ids)
         torch.cuda.synchronize()
         got = [u64(x) for x in dig.cpu().tolist()]
         for s in sample:
             want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
-            assert np.array_equal(parts[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), (kern, s)
-            assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], (kern, s)
+            assert np.array_equal(parts[s * n:(s + 1) * n, :ps].cpu().numpy(), np.stack(want)), (kern, pf, s)
+            assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], (kern, pf, s)
     avail = dev(synth.batch_survivors(S, n, k, first=4242))
     for kern in ("slice", "run"):
         with _tuned(dec_kernel=_dec(kern)):

@@ -27,6 +27,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
 ap.add_argument("--json")
 ap.add_argument("--config")
+ap.add_argument("--stripes", type=int, default=0, help="per-GPU stripes of the profiled run (bench --stripes)")
 a = ap.parse_args()
 out = {}
 for d in a.dirs:
@@ -54,9 +55,10 @@ if a.json and a.config:
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import CONFIGS
-    rec["stripes"] = CONFIGS[a.config][0]  # bench.py uses the figure only for this batch size
+    # bench.py uses the figure only for this per-GPU batch size
+    rec["stripes"] = a.stripes or CONFIGS[a.config][0]
     doc = {}
     if os.path.exists(a.json):
         doc = json.load(open(a.json))
-    doc[a.config] = rec
+    doc[f"{a.config}@{a.stripes}" if a.stripes else a.config] = rec
     json.dump(doc, open(a.json, "w"), indent=1, sort_keys=True)
