@@ -69,7 +69,9 @@ enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_G
  * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16);
  * NKFS_DEC_RUN: run decoder (k <= 8: persistent waves, each walking one
  * contiguous run of 1,024-row units across stripes) */
-enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG, NKFS_DEC_RUN };
+/* NKFS_DEC_PAIR: k = 2 decoder (closed-form 2 x 2 inverse, one lookup per row) */
+enum { NKFS_DEC_AUTO = 0, NKFS_DEC_SLICE, NKFS_DEC_WAVE, NKFS_DEC_GENERIC, NKFS_DEC_WIDE, NKFS_DEC_BIG, NKFS_DEC_RUN,
+       NKFS_DEC_PAIR };
 struct nkfs_tune {
 	int enc_kernel;       /* NKFS_ENC_*: encoder (WIDE / GENERIC also pin n <= 8 shapes) */
 	int dec_kernel;       /* NKFS_DEC_*: decoder (WIDE / GENERIC also pin k <= 8) */
@@ -84,6 +86,11 @@ struct nkfs_tune {
 	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
 	int dec_run_units;    /* run decoder: 1,024-row units per chunk (1, 2, 4, 8, 16) */
 	int enc_ws_prefetch;  /* warp-specialised encoder, n > 4: chunks of loads in flight per encoder wave (1, 2) */
+	int enc_big_unfused;  /* k > 16 encoder: 1 = XXH64 as a second pass over the parts (0 = fused, default) */
+	int dec_pair_stage;   /* k = 2 decoder: 1 = output through an LDS stage (1 KiB runs per store), 0 = direct */
+	int host_depth;       /* host-memory entry points: sub-batches in flight per lane (2..8) */
+	int host_lanes;       /* host-memory entry points: host threads (lanes) per device (1..4) */
+	int enc_ragged_split; /* ragged n > 4 encode: parts >= this many bytes on the warp-specialised kernel (0 = all walk) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

@@ -35,11 +35,12 @@ class Tune(C.Structure):
     _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
                                        "dec_units", "enc_nib", "enc_units", "size_order", "enc_prefetch",
                                        "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units",
-                                       "enc_ws_prefetch")]
+                                       "enc_ws_prefetch", "enc_big_unfused", "dec_pair_stage",
+                                       "host_depth", "host_lanes", "enc_ragged_split")]
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4, "wide": 5, "big": 6, "wide_ws": 7}
-DEC = {"auto": 0, "slice": 1, "wave": 2, "generic": 3, "wide": 4, "big": 5, "run": 6}
+DEC = {"auto": 0, "slice": 1, "wave": 2, "generic": 3, "wide": 4, "big": 5, "run": 6, "pair": 7}
 
 # name -> (restype, argtypes)
 _SIGS = {

@@ -33,8 +33,10 @@
 //                rows' 16 columns, and the
 //                groups of a (stripe, slice) run back to back on one XCD so
 //                the rows' lines complete in its L2.
-// XXH64 of the parts is the batched message hash afterwards (a part's chain
-// is serial over all of its rows, and a stripe's rows are spread over slices).
+// XXH64 of the parts is fused into k_encode_big: a part's chain is serial over
+// all of its rows and a stripe's rows are spread over slices, so slice i's
+// workgroup continues the 64 chains of its part group from the accumulators
+// slice i-1's workgroup published (BigChain, below).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
@@ -42,6 +44,10 @@
 #include <type_traits>
 
 #include "nk8_dev.h"
+#include "nkfs_internal.h"
+#include "runtime.h"
+#include "scratch.h"
+#include "xxh64_dev.h"
 
 using namespace nkfs;
 using namespace nkfs::dev;
@@ -67,21 +73,41 @@ __device__ inline u32 gf_pow(const uint16_t *lg, const u8 *ex, u32 x, u32 e)
     return ex[(u32(lg[x]) * e) % 255u];
 }
 
+// Chain hand-off of the fused XXH64 (HASH): one record per (stripe, group of
+// 16 parts) -- the 64 accumulators (16 parts x 4) after the slices folded so
+// far and a flag = the number of slices folded (agent-scope release/acquire).
+struct BigChain {
+    u64 *acc;       // [units][64]
+    u32 *flag;      // [units], zeroed before the launch
+    u32 *fail;      // set when a wait timed out: k_big_hash_fix recomputes the digests
+    u64 *digests;   // [stripe][n]
+};
+
+constexpr u64 CHAIN_TIMEOUT = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
+
+template <bool HASH>
 __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *ids, const GfTables *gft,
-                                                       u32 ngroups, u32 nslices)
+                                                       u32 ngroups, u32 nslices, BigChain ch)
 {
     __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];   // 16 tables of 256 x 16 B
     __shared__ __attribute__((aligned(16))) u32 stage[4 * 256];      // [part quad][row]
     __shared__ __attribute__((aligned(16))) uint4 coef[256];         // coef[m] = (x_{p0+e}^m), e < 16
+    __shared__ __attribute__((aligned(16))) u8 hx[HASH ? 16 * 256 : 16];  // [part][row] of a 256-row unit
     __shared__ uint16_t glog[256];
     __shared__ u8 gexp[256];
 
+    // workgroup b runs on XCD b mod 8; slice-major over (slice, stripe octet,
+    // group): the groups of a (stripe, slice) run back to back on one XCD
+    // (they share the block's lines in its L2), and slice i of a (stripe,
+    // group) is dispatched 8 * ngroups * octets workgroups after slice i-1,
+    // on the same XCD (the XXH64 chain hand-off below waits on it)
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
+    const u32 noct = (g.nstripes + 7) / 8;
     const u32 grp = loc % ngroups;
-    const u32 slice = (loc / ngroups) % nslices;
-    const u32 s = (loc / ngroups / nslices) * 8 + (b & 7);
-    if (s >= g.nstripes)
+    const u32 slice = loc / (ngroups * noct);
+    const u32 s = ((loc / ngroups) % noct) * 8 + (b & 7);
+    if (s >= g.nstripes || slice >= nslices)
         return;  // the whole workgroup: no barrier is skipped by part of it
     const Stripe v = stripe_at(g, s);
     const u32 r_begin = slice * ENC_ROWS;
@@ -204,11 +230,46 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             rows(std::false_type{});
     }
 
+    // XXH64 of the group's parts, fused (HASH): wave 0's lane 4e + a is
+    // accumulator a of part p0 + e.  The chain of a part is serial over all
+    // its rows, so slice i continues from the accumulators slice i-1's
+    // workgroup published (dispatched earlier on this XCD, normally long
+    // done); each 256-row unit is folded from an LDS [part][row] copy of its
+    // outputs while the unit is stored
+    const int he = lane >> 2, ha = lane & 3;
+    const u32 unit = s * ngroups + grp;
+    const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
+    const u32 last = (v.ps - 1) / ENC_ROWS;
+    u64 hacc = 0;
+    bool hok = true;
+    if (HASH && wave == 0) {
+        hacc = xxh_acc_init(ha, 0);
+        if (slice > 0) {
+            const u64 t0 = __builtin_amdgcn_s_memrealtime();
+            u32 f;
+            for (;;) {
+                f = __hip_atomic_load(ch.flag + unit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (f >= slice || __hip_atomic_load(ch.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_TIMEOUT) {
+                    if (lane == 0)
+                        __hip_atomic_store(ch.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            hok = f >= slice && f != 0xFFFFFFFFu;
+            if (hok)
+                hacc = ch.acc[u64(unit) * 64 + lane];
+        }
+    }
+
     // 256 rows x 16 parts per t-unit: [part quad][row] in LDS (conflict-free
     // dword writes), read back as 4 rows x 4 parts (ds_read_b128), 4x4 byte
     // transpose, one dword of 4 rows per part: wave w stores parts
     // 4w..4w+3, 64 lanes x 4 B = 256 contiguous bytes per instruction
     const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
+    u64 tw[4] = {0, 0, 0, 0};  // a part's tail bytes (< 32), for its digest
 #pragma unroll
     for (int t = 0; t < ENC_T; ++t) {
         const u32 rt = r_begin + u32(t) * 256u;
@@ -227,6 +288,8 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int e = 4 * wave + j;
+            if constexpr (HASH)
+                *reinterpret_cast<u32 *>(hx + e * 256 + 4 * lane) = o[j];
             if (e < np && rr < v.ps) {
                 u8 *dst = v.parts + u64(p0 + e) * v.pitch + rr;
                 if (pal && rr + 4u <= v.ps) {
@@ -237,7 +300,92 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                 }
             }
         }
+        if constexpr (HASH) {
+            __syncthreads();
+            if (wave == 0) {
+                // rounds of the 32-byte stripes that lie wholly below ps
+                const u8 *src = hx + he * 256 + 8 * ha;
+                const u32 s0 = rt >> 5;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const u64 w = *reinterpret_cast<const u64 *>(src + 32 * r);
+                    const u64 nx = xxh_round(hacc, w);
+                    hacc = s0 + u32(r) < nst ? nx : hacc;
+                }
+                // the tail (ps & 31 bytes after the last whole stripe) lies
+                // in this unit: keep its words for the digest
+                if ((v.ps & 31) && nst * 32 >= rt && nst * 32 < rt + 256) {
+                    const u64 *tp = reinterpret_cast<const u64 *>(hx + he * 256 + (nst * 32 - rt));
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        tw[w] = tp[w];
+                }
+            }
+        }
     }
+    if constexpr (HASH) {
+        if (wave == 0) {
+            if (slice < last) {
+                // publish: the accumulators, then the flag (agent-scope
+                // release); a chain that could not be continued passes the
+                // failure on at once so no successor waits for it
+                ch.acc[u64(unit) * 64 + lane] = hacc;
+                if (lane == 0)
+                    __hip_atomic_store(ch.flag + unit, hok ? slice + 1 : 0xFFFFFFFFu, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const int base = lane & ~3;
+                const u64 v1 = shfl64(hacc, base), v2 = shfl64(hacc, base + 1);
+                const u64 v3 = shfl64(hacc, base + 2), v4 = shfl64(hacc, base + 3);
+                if (hok && ha == 0 && he < np) {
+                    u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+                    h += v.ps;
+                    ch.digests[u64(s) * u64(n) + u64(p0 + he)] = xxh_tail_regs(h, tw, v.ps & 31);
+                }
+            }
+        }
+    }
+}
+
+// The fused hash's safety net: when a chain wait timed out (ch.fail; not
+// expected -- slice i-1 is dispatched long before slice i on the same XCD),
+// every part's digest is recomputed here, four lanes per part; otherwise
+// every workgroup returns at once.
+__global__ __launch_bounds__(256) void k_big_hash_fix(nkfs_geom g, const u32 *fail, u64 *digests)
+{
+    if (!__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return;
+    const u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x;
+    const u64 msg = t >> 2;
+    const int a = int(t & 3);
+    const bool live = msg < u64(g.nstripes) * u64(g.n);
+    const u8 *p = nullptr;
+    u32 len = 0;
+    if (live) {
+        const u32 s = u32(msg / u32(g.n)), i = u32(msg % u32(g.n));
+        const Stripe v = stripe_at(g, s);
+        p = v.parts + u64(i) * v.pitch;
+        len = v.ps;
+    }
+    u64 acc = xxh_acc_init(a, 0);
+    const u32 nst = len >> 5;
+    for (u32 r = 0; r < nst; ++r) {
+        u64 w = 0;
+        for (int c = 0; c < 8; ++c)  // ragged part bases: byte loads
+            w |= u64(p[u64(r) * 32 + 8 * a + c]) << (8 * c);
+        acc = xxh_round(acc, w);
+    }
+    const int base = int(threadIdx.x & 63) & ~3;
+    const u64 v1 = shfl64(acc, base), v2 = shfl64(acc, base + 1);
+    const u64 v3 = shfl64(acc, base + 2), v4 = shfl64(acc, base + 3);
+    if (!live || a != 0)
+        return;
+    u64 h = len >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+    h += len;
+    u64 tw[4] = {0, 0, 0, 0};
+    for (u32 c = 0; c < (len & 31); ++c)
+        tw[c >> 3] |= u64(p[u64(nst) * 32 + c]) << (8 * (c & 7));
+    digests[msg] = xxh_tail_regs(h, tw, len & 31);
 }
 
 // Up to 4 bytes (left >= 1; fewer when left < 4) from an unaligned address,
@@ -430,10 +578,13 @@ __global__ __launch_bounds__(256, 2) void k_decode_big(nkfs_geom g, const u8 *wo
 
 }  // namespace
 
-// Encode (no hash) a uniform or ragged batch with any 2 <= k <= 254, n <= 255
-// through 16-column chunks.  -ENOSYS where a stripe's buffer offsets would
-// not fit 31 bits.
-extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const void *gf, hipStream_t st)
+// Encode a uniform or ragged batch with any 2 <= k <= 254, n <= 255 through
+// 16-column chunks, with the XXH64 of every part fused when `digests` is
+// given (the chain hand-off records live in the launch's scratch,
+// scratch.h).  -ENOSYS where a stripe's buffer offsets would not fit 31 bits
+// (or no scratch could be had for the hand-off: the caller hashes after).
+extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
+                               hipStream_t st)
 {
     const int k = g->k;
     if (k < 2 || k > 254 || g->n < k || g->n > 255)
@@ -448,9 +599,31 @@ extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const voi
     const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
-    hipLaunchKernelGGL(k_encode_big, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
-                       u32(ngroups), u32(nslices ? nslices : 1));
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    if (!digests) {
+        hipLaunchKernelGGL(k_encode_big<false>, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
+                           u32(ngroups), u32(nslices ? nslices : 1), BigChain{});
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
+    // hand-off records: per (stripe, group) 64 accumulators + a flag, and the failure word
+    const u64 units = u64(g->nstripes) * ngroups;
+    const u64 acc_b = (units * 64 * 8 + 255) & ~u64(255), flag_b = (units * 4 + 4 + 255) & ~u64(255);
+    Scratch sc;
+    u8 *rec = static_cast<u8 *>(sc.take(g, acc_b + flag_b, st));
+    if (!rec)
+        return -ENOSYS;
+    BigChain ch{reinterpret_cast<u64 *>(rec), reinterpret_cast<u32 *>(rec + acc_b),
+                reinterpret_cast<u32 *>(rec + acc_b) + units, digests};
+    int rc = hipMemsetAsync(ch.flag, 0, units * 4 + 4, st) == hipSuccess ? 0 : -EIO;
+    if (!rc) {
+        hipLaunchKernelGGL(k_encode_big<true>, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
+                           u32(ngroups), u32(nslices ? nslices : 1), ch);
+        const u64 threads = u64(g->nstripes) * u64(g->n) * 4;
+        hipLaunchKernelGGL(k_big_hash_fix, dim3(u32((threads + 255) / 256)), dim3(256), 0, st, *g,
+                           (const u32 *)ch.fail, digests);
+        rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
+    const int e = sc.finish();
+    return rc ? rc : e;
 }
 
 // Decode a uniform or ragged batch with 2 <= k <= 254 from the plan

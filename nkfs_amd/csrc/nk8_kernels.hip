@@ -647,13 +647,16 @@ extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests,
                                 int cus, hipStream_t st);
 extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st);
 extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st);
-extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, const void *gf, hipStream_t st);
+extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
+                               hipStream_t st);
 extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                  void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                  hipStream_t st);
+extern "C" int nkfs_pair_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
+                                int navail, int32_t *status, const void *gf, int xp, hipStream_t st);
 extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                hipStream_t st);
@@ -687,6 +690,22 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
     const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
                      : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
                                                                   : NKFS_ENC_AUTO;
+    if (kern == NKFS_ENC_WALK && g->block_sizes && digests && g->n > 4 && t.enc_ragged_split &&
+        !g->part_min && !g->part_max) {
+        // ragged n > 4: stripes with parts of at least enc_ragged_split bytes
+        // on the warp-specialised kernel (C3's), the rest on the walk
+        // encoder; two launches over the same size order with complementary
+        // part-size windows (nkfs_geom.part_min / part_max)
+        nkfs_geom big = *g, small = *g;
+        big.part_min = u32(t.enc_ragged_split);
+        small.part_max = u32(t.enc_ragged_split);
+        int rc = nkfs_ws_encode(&big, ids, digests, 4, false, st);
+        if (!rc)
+            rc = nkfs_walk_encode(&small, ids, digests, 1, t.enc_nib < 0 ? 0 : t.enc_nib, t.enc_waves_per_cu,
+                                  nkfs_cu_count(), st);
+        if (rc != -ENOSYS)
+            return rc;
+    }
     if (kern == NKFS_ENC_WALK) {
         // two 1,024-row units per chunk for n <= 4 (a 4 KiB N4K2 stripe is one chunk)
         const int units = g->n <= 4 ? (t.enc_units ? t.enc_units : 2) : 1;
@@ -737,12 +756,17 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         if (rc != -ENOSYS)
             return rc;
     }
-    // else part groups of 8 for k <= 16, 16-column chunks beyond
-    // (nk8_big.hip), then the batched XXH64 of the parts
+    // else part groups of 8 for k <= 16 (then the batched XXH64 of the
+    // parts), 16-column chunks beyond (nk8_big.hip, XXH64 fused unless
+    // nkfs_tune.enc_big_unfused asks for the second pass)
     if (kern != NKFS_ENC_GENERIC) {
         rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
-        if (rc == -ENOSYS)
-            rc = nkfs_big_encode(g, ids, gf, st);
+        if (rc != -ENOSYS)
+            return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
+        rc = digests && !nkfs_tune_now().enc_big_unfused ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
+        if (rc != -ENOSYS)
+            return rc;
+        rc = nkfs_big_encode(g, ids, nullptr, gf, st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
     }
@@ -799,6 +823,14 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
                          : small_k2                            ? NKFS_DEC_WAVE
                          : g->block_sizes && g->nstripes >= 2048 ? NKFS_DEC_RUN
                                                                  : NKFS_DEC_SLICE;
+        if (kern == NKFS_DEC_PAIR && !expect) {
+            auto pair = [&](const nkfs_geom *go) {
+                return nkfs_pair_decode(go, n_slots, ids, avail, navail, status, gf, t.dec_pair_stage, st);
+            };
+            rc = with_size_order(g, st, pair);
+            if (rc == -ENOSYS)
+                rc = pair(g);
+        }
         if (kern == NKFS_DEC_RUN && !expect)
             rc = nkfs_run_decode(g, n_slots, ids, avail, navail, work, status, gf, t.dec_run_units, t.dec_waves_per_cu,
                                  nkfs_cu_count(), st);

@@ -315,7 +315,7 @@ static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
 
 /* ------------------------------------------------------------ sub-batches */
 
-#define NSTREAM 3
+#define NSTREAM_MAX 8 /* contexts (sub-batches in flight) per lane: struct nkfs_tune.host_depth */
 
 /* Device / pinned scratch layout of one sub-batch of at most `cnt` stripes
  * (offsets into the context buffers). */
@@ -806,7 +806,8 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 		max_scr = sb > max_scr ? sb : max_scr;
 		s = u.s1;
 	}
-	struct ctxs xs[NSTREAM];
+	const int NSTREAM = nkfs_host_depth();
+	struct ctxs xs[NSTREAM_MAX];
 	memset(xs, 0, sizeof(xs));
 	int rc = 0;
 	for (int i = 0; i < NSTREAM; i++) {
@@ -830,7 +831,7 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 	/* stages per context: issue -> (decode) copy_blocks -> retire, with up
 	 * to three sub-batches in flight: sub-batch i is issued, i-1's blocks
 	 * are copied back once its status is known, i-2 retires */
-	struct ctxs *ring[NSTREAM] = {0};
+	struct ctxs *ring[NSTREAM_MAX] = {0};
 	uint32_t it = 0;
 	for (uint32_t s = s0; s < s1 && !rc; it++) {
 		struct ctxs *x = &xs[it % NSTREAM];
@@ -854,7 +855,7 @@ static int run_lane(const struct hp *h, int dev, uint32_t s0, uint32_t s1)
 		s = x->u.s1;
 	}
 	/* drain in issue order */
-	for (uint32_t j = 0; j < NSTREAM; j++) {
+	for (uint32_t j = 0; j < (uint32_t)NSTREAM; j++) {
 		struct ctxs *x = &xs[(it + j) % NSTREAM];
 		if (!x->u.live)
 			continue;
@@ -908,6 +909,18 @@ static int hp_run(struct hp *h)
 		return rc;
 	int lanes[NKFS_MAX_DEVICES];
 	int nl = nkfs_gpu_get_devices(lanes, NKFS_MAX_DEVICES);
+	/* struct nkfs_tune.host_lanes host threads per device: each lane keeps
+	 * its own host_depth sub-batches in flight, so one host thread blocked
+	 * on a stream never leaves the link idle */
+	const int per = nkfs_host_lanes();
+	if (per > 1) {
+		int dv[NKFS_MAX_DEVICES], nd = nl;
+		memcpy(dv, lanes, sizeof(dv));
+		nl = 0;
+		for (int i = 0; i < nd; i++)
+			for (int j = 0; j < per && nl < NKFS_MAX_DEVICES; j++)
+				lanes[nl++] = dv[i];
+	}
 	if (nl > (int)h->nstripes)
 		nl = (int)h->nstripes;
 	if (nl <= 1) {

@@ -61,6 +61,9 @@ static struct nkfs_tune g_tune = {
 	.dec_wave_waves_per_cu = 0,
 	.dec_run_units = 4,
 	.enc_ws_prefetch = 1,
+	.dec_pair_stage = 1,
+	.host_depth = 3,
+	.host_lanes = 1,
 };
 
 void nkfs_tune_get(struct nkfs_tune *t)
@@ -75,7 +78,7 @@ void nkfs_tune_get(struct nkfs_tune *t)
 int nkfs_tune_set(const struct nkfs_tune *t)
 {
 	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WIDE_WS || t->dec_kernel < NKFS_DEC_AUTO ||
-	    t->dec_kernel > NKFS_DEC_RUN || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
+	    t->dec_kernel > NKFS_DEC_PAIR || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
 	    t->enc_units < 0 || t->enc_units > 2 ||
@@ -84,12 +87,28 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)) ||
 	    (t->dec_run_units != 1 && t->dec_run_units != 2 && t->dec_run_units != 4 && t->dec_run_units != 8 &&
 	     t->dec_run_units != 16) ||
-	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2)
+	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_unfused != 0 && t->enc_big_unfused != 1) ||
+	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
+	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;
 	pthread_mutex_unlock(&g_tune_lock);
 	return 0;
+}
+
+int nkfs_host_depth(void)
+{
+	struct nkfs_tune t;
+	nkfs_tune_get(&t);
+	return t.host_depth;
+}
+
+int nkfs_host_lanes(void)
+{
+	struct nkfs_tune t;
+	nkfs_tune_get(&t);
+	return t.host_lanes;
 }
 
 int nkfs_hip_fail(const char *what, int err)
@@ -358,7 +377,7 @@ struct nkfs_ctx *nkfs_ctx_get(void)
 	return ready_now() ? nkfs_ctx_get_on(g_device) : NULL;
 }
 
-#define POOL_KEEP 16
+#define POOL_KEEP 32 /* >= host_lanes x host_depth at their maxima */
 
 void nkfs_ctx_put(struct nkfs_ctx *c)
 {

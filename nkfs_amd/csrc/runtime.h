@@ -36,5 +36,7 @@ void nkfs_gpu_release(void);
 void nkfs_ctx_trim(void);
 int nkfs_bad_params(uint32_t block_size, int n, int k);
 int nkfs_hip_fail(const char *what, int err);
+int nkfs_host_depth(void); /* struct nkfs_tune.host_depth: sub-batches in flight per lane */
+int nkfs_host_lanes(void); /* struct nkfs_tune.host_lanes: host lanes per device */
 
 #endif

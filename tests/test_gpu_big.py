@@ -169,14 +169,27 @@ def test_big_decode_matches(L, O, n, k, B, S):
     assert np.array_equal(np.asarray(got), ref[s].numpy())
 
 
-def test_big_round_trip_w2(L):
-    """The bench's W2 batch (256 x 1 MiB, N48K32): default encode -> keep 32
-    seeded survivors -> default decode gives every block back."""
-    from nkfs_amd import batch
+def test_big_round_trip_w2(L, O):
+    """The bench's W2 batch (256 x 1 MiB, N48K32): default encode (XXH64
+    fused, each slice continuing its part group's chains from the previous
+    slice's workgroup) gives the same parts and digests as the encoder with
+    the separate hash pass, the oracle's digests on a sample; keep 32 seeded
+    survivors -> default decode gives every block back."""
+    from nkfs_amd import _lib, batch
     S, B, n, k = 256, 1048576, 48, 32
     blocks = batch.synth(S, B, first=11)
-    ids = dev(synth.batch_ids(S, n, first=11))
-    parts, _ = batch.encode(blocks, B, n, k, ids)
+    ids_np = synth.batch_ids(S, n, first=11)
+    ids = dev(ids_np)
+    parts, dig = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_big_unfused=1):
+        parts1, dig1 = batch.encode(blocks, B, n, k, ids)
+    torch.cuda.synchronize()
+    assert torch.equal(parts, parts1) and torch.equal(dig, dig1)
+    del parts1
+    got = [u64(x) for x in dig.cpu().tolist()]
+    for s in (0, 137, S - 1):
+        want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
+        assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
     avail = dev(synth.batch_survivors(S, n, k, first=11))
     out, status = batch.decode(parts, n, ids, avail, k, B)
     torch.cuda.synchronize()

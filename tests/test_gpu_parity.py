@@ -912,3 +912,80 @@ def test_run_decode_walks_across_stripes(L, O, n, k, waves, units):
         out, status = batch.decode(up, n, dev(uid), uav, k, B)
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0 and torch.equal(out, blocks[:, :B])
+
+
+@pytest.mark.parametrize("n,B,S", [(4, 4096, 3000), (4, 1, 9), (3, 3, 40), (6, 4097, 77), (4, 65536 * 2 + 7, 9),
+                                   (255, 2048 * 4 + 1, 5), (2, 1048576, 3)])
+def test_pair_decode_matches(L, O, n, B, S):
+    """The k = 2 decoder (nk8_pair.hip: d1 = (p_a ^ p_b) / (x_a ^ x_b),
+    d0 = p_a ^ x_a d1 from one product-table lookup per row) rebuilds the
+    same blocks as the wave decoder and the oracle, with and without its
+    output stage: every slot offered (the survivors first), stripe 1's second
+    offer repeating the first one's id (the selection takes the next distinct
+    one, crt/nk8.c:512-537), stripe 2 offering a single distinct id (status
+    -EINVAL, block untouched); odd block sizes and tails of every length, long
+    stripes split into row slices."""
+    from nkfs_amd import batch
+    k = 2
+    blocks = batch.synth(S, B, first=21)
+    ids_np = synth.batch_ids(S, n, first=21)
+    parts, _ = batch.encode(blocks, B, n, k, dev(ids_np))
+    av = synth.batch_survivors(S, n, k, first=21)
+    av = np.stack([np.concatenate([r, [j for j in range(n) if j not in r]]) for r in av]).astype(np.uint8)
+    ids2 = ids_np.copy()
+    if S > 2:
+        ids2[1, av[1, 1]] = ids2[1, av[1, 0]]
+        ids2[2, :] = ids2[2, 0]
+    outs = []
+    for kern, stage in (("wave", 1), ("pair", 1), ("pair", 0)):
+        with _tuned(dec_kernel=_dec(kern), dec_pair_stage=stage):
+            out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
+            _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
+            torch.cuda.synchronize()
+            outs.append((out.clone(), st.cpu().tolist()))
+    for o, st in outs[1:]:
+        assert st == outs[0][1]
+        assert torch.equal(o, outs[0][0])
+    o, st = outs[1]
+    for s in range(S):
+        if s == 2 or (s == 1 and n == k):
+            continue
+        assert st[s] == 0 and torch.equal(o[s], blocks[s, :B]), s
+    if S > 2:
+        assert st[2] == -22 and bool((o[2] == 0xEE).all())
+    # the oracle's assemble of the last stripe from its first two offers
+    s = S - 1
+    sel = [int(x) for x in av[s][:2]]
+    pn = parts[s * n:(s + 1) * n, :batch.part_size(B, k)].cpu().numpy()
+    assert np.array_equal(np.asarray(O.decode([pn[j] for j in sel], ids_np[s][sel], k, B)), blocks[s, :B].cpu().numpy())
+
+
+@pytest.mark.parametrize("gap,stage", [(0, 1), (3, 1), (5, 0)])
+def test_pair_decode_ragged(L, gap, stage):
+    """The k = 2 decoder on a ragged batch (size order applied, blocks at
+    unaligned offsets): every stripe back bit-exact, gap bytes untouched."""
+    from nkfs_amd import batch
+    n, k = 4, 2
+    sizes = synth.mixed_sizes(40)
+    sizes[:5] = (4096, 1, 3, 1048576, 70001)
+    boff, poff, pos, ppos = _ragged_layout(sizes, n, k, gap)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(700 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=700)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff),
+                        None, int(sizes.max()))
+    avail = synth.batch_survivors(len(sizes), n, 3, first=700)
+    out = torch.zeros(pos + 16, dtype=torch.uint8, device="cuda")
+    with _tuned(dec_kernel=_dec("pair"), dec_pair_stage=stage):
+        status = batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(avail), k, out, dev(boff),
+                                     dev(sizes.astype(np.int32)), int(sizes.max()))
+    torch.cuda.synchronize()
+    assert status.abs().sum().item() == 0
+    got = out.cpu().numpy()
+    mask = np.ones(pos + 16, bool)
+    for s, B in enumerate(sizes):
+        assert np.array_equal(got[boff[s]: boff[s] + B], host[boff[s]: boff[s] + B]), (s, int(B))
+        mask[boff[s]: boff[s] + B] = False
+    assert not got[mask].any()

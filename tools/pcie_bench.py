@@ -3,7 +3,14 @@ the path's real ends, SURVEY.md §8(f) row 2.  User bytes (block bytes) per
 second, host buffers pinned once (a server's page pool), outputs verified
 against the inputs after timing.
 
-    python tools/pcie_bench.py [c2 c3 c4 c5 pages lanes]
+    python tools/pcie_bench.py [link c2 c3 c4 c5 pages lanes depth]
+
+link  = the raw pinned link on this box: hipMemcpyAsync H2D alone, D2H alone,
+        and both at once on two streams (1 GiB each way); every PUT / GET line
+        then carries the bound the link puts on it (user GiB/s such that the
+        H2D bytes, the D2H bytes and their sum each fit the measured rates)
+        and the fraction of it reached.
+depth = C3 PUT / GET at host_depth 3 / 6 x host_lanes 1 / 2 (struct nkfs_tune)
 
 PUT  = nkfs_nk8_encode_host: blocks H2D -> encode + XXH64 -> parts + digests D2H
 GET  = nkfs_nk8_decode_host: k survivor parts per stripe H2D -> decode -> blocks D2H
@@ -25,6 +32,61 @@ from bench import C5_SIZES, CONFIGS  # noqa: E402
 from nkfs_amd import _lib, batch, synth  # noqa: E402
 
 GIB = 2**30
+LINK = {}
+
+
+def link():
+    """Raw pinned PCIe rates (GiB/s): H2D, D2H, and both directions at once."""
+    nbytes = 1 << 30
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def run(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+
+    LINK["h2d"] = nbytes / run(h2d) / GIB
+    LINK["d2h"] = nbytes / run(d2h) / GIB
+    t = run(both)
+    LINK["bidir_total"] = 2 * nbytes / t / GIB
+    print(f"link (pinned, 1 GiB)  H2D {LINK['h2d']:6.2f} GiB/s   D2H {LINK['d2h']:6.2f} GiB/s   "
+          f"both at once {LINK['bidir_total']:6.2f} GiB/s in all", flush=True)
+    del h, h2, d, d2
+
+
+def bound(h2d_per_user, d2h_per_user):
+    """User GiB/s the measured link allows when every user byte moves
+    h2d_per_user bytes host->device and d2h_per_user bytes device->host."""
+    if not LINK:
+        return None
+    return min(LINK["h2d"] / h2d_per_user, LINK["d2h"] / d2h_per_user,
+               LINK["bidir_total"] / (h2d_per_user + d2h_per_user))
+
+
+def frac(rate, b):
+    return f"{rate / b:5.3f}" if b else "  n/a"
 
 
 def timed(fn, reps=3):
@@ -36,7 +98,7 @@ def timed(fn, reps=3):
     return (time.perf_counter() - t0) / reps
 
 
-def uniform(name, user_bytes=1 << 30, lanes=None):
+def uniform(name, user_bytes=1 << 30, lanes=None, tune=None):
     S0, B, n, k, _ = CONFIGS[name]
     S = min(S0, user_bytes // B)
     pitch = batch.part_pitch(B, k)
@@ -46,6 +108,8 @@ def uniform(name, user_bytes=1 << 30, lanes=None):
     dig = torch.empty(S * n, dtype=torch.int64).pin_memory()
     if lanes is not None:
         _lib.check(batch.set_devices(lanes))
+    tuned = _lib.tuned(**(tune or {}))
+    tuned.__enter__()
     t_put = timed(lambda: batch.encode_host(blocks, B, n, k, ids, out=(parts, dig)))
     # GET: the k survivors each stripe holds, packed (n_slots = k)
     surv = synth.batch_survivors(S, n, k).astype(np.int64)
@@ -63,13 +127,19 @@ def uniform(name, user_bytes=1 << 30, lanes=None):
     t_getv = timed(lambda: batch.decode_host(held, pitch, k, hid, avail, k, k, B, out, B, status=st, expect=hexp,
                                              badmask=bad))
     ok = ok and bool(torch.equal(out, blocks)) and int(st.abs().sum()) == 0
+    tuned.__exit__(None, None, None)
     if lanes is not None:
         batch.set_devices([])
     ub = S * B
     tag = f"{name} lanes={lanes}" if lanes is not None else name
-    print(f"{tag:18s} {S:6d} x {B:8d}  PUT {ub / t_put / GIB:6.2f} GiB/s   GET {ub / t_get / GIB:6.2f} GiB/s   "
-          f"GET+verify {ub / t_getv / GIB:6.2f} GiB/s   in/out per GiB user: PUT {1 + n * pitch / B:.2f} GiB, "
-          f"GET {1 + k * pitch / B:.2f} GiB   verified={ok}", flush=True)
+    if tune:
+        tag += " " + ",".join(f"{a}={b}" for a, b in tune.items())
+    put, get, getv = ub / t_put / GIB, ub / t_get / GIB, ub / t_getv / GIB
+    bp, bg = bound(1.0, n * pitch / B), bound(k * pitch / B, 1.0)
+    print(f"{tag:18s} {S:6d} x {B:8d}  PUT {put:6.2f} GiB/s   GET {get:6.2f} GiB/s   "
+          f"GET+verify {getv:6.2f} GiB/s   in/out per GiB user: PUT {1 + n * pitch / B:.2f} GiB, "
+          f"GET {1 + k * pitch / B:.2f} GiB   link bound PUT {bp or 0:6.2f} ({frac(put, bp)}) "
+          f"GET {bg or 0:6.2f} ({frac(get, bg)})   verified={ok}", flush=True)
 
 
 def ragged(user_bytes=1 << 30, pages=False, page=4096):
@@ -101,8 +171,12 @@ def ragged(user_bytes=1 << 30, pages=False, page=4096):
         out = torch.zeros(pos, dtype=torch.uint8).pin_memory()
         t_get = timed(lambda: batch.decode_ragged_host(parts, po, n, ids, avail, k, k, out, bo, sz, status=st))
         ok = bool(torch.equal(out, host)) and int(st.abs().sum()) == 0
-        print(f"c5 ragged          {S:6d} stripes  PUT {ub / t_put / GIB:6.2f} GiB/s   GET {ub / t_get / GIB:6.2f} GiB/s"
-              f"   (GET ships all {n} slots)   verified={ok}", flush=True)
+        ps_all = float(n * sum(batch.part_pitch(B, k) for B in sizes.tolist())) / ub
+        bp, bg = bound(1.0, ps_all), bound(ps_all, 1.0)
+        put, get = ub / t_put / GIB, ub / t_get / GIB
+        print(f"c5 ragged          {S:6d} stripes  PUT {put:6.2f} GiB/s   GET {get:6.2f} GiB/s"
+              f"   (GET ships all {n} slots)   link bound PUT {bp or 0:6.2f} ({frac(put, bp)}) "
+              f"GET {bg or 0:6.2f} ({frac(get, bg)})   verified={ok}", flush=True)
         return
     # page lists: every block in its own 4 KiB pages of a pinned pool
     npg = [(B + page - 1) // page for B in sizes.tolist()]
@@ -133,9 +207,15 @@ def ragged(user_bytes=1 << 30, pages=False, page=4096):
 def main():
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(0))
-    what = sys.argv[1:] or ["c2", "c3", "c4", "c5", "pages", "lanes"]
+    what = sys.argv[1:] or ["link", "c2", "c3", "c4", "c5", "pages", "lanes", "depth"]
     for w in what:
-        if w in ("c2", "c3", "c4"):
+        if w == "link":
+            link()
+        elif w == "depth":
+            for depth in (3, 6):
+                for lanes_per in (1, 2):
+                    uniform("c3", tune={"host_depth": depth, "host_lanes": lanes_per})
+        elif w in ("c2", "c3", "c4"):
             uniform(w)
         elif w == "c5":
             ragged()
