@@ -367,25 +367,69 @@ def roofline(kernel, nbytes, secs, traffic):
 
 # --------------------------------------------------------------- workload
 
+def workload(name, rank, world, stripes=0, strong_total=0):
+    """(first global stripe, stripes on this rank, workload label) of a
+    uniform config: strong scaling splits strong_total stripes over the
+    ranks, weak scaling gives every rank `stripes` (default the config's)."""
+    S, B, n, k, desc = CONFIGS[name]
+    head = desc.split(", ")[0]  # "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased)"
+    if strong_total:
+        first, S = strong_range(rank, world, strong_total)
+        return first, S, (f"{head}, {strong_total} x {B // 1024} KiB stripes in all, split evenly over {world} "
+                          f"GPU(s) (strong scaling; {S} on this GPU)")
+    if stripes:
+        S = stripes
+        desc = f"{head}, {S} x {B // 1024} KiB stripes per GPU"
+    elif world > 1:
+        desc = f"{desc} (weak scaling: {S * world} in all over {world} GPUs)"
+    first, _ = stripe_range(rank, S)
+    return first, S, desc
+
+
+def uniform_result(name, args, rank, world, device, S, B, n, k, desc, strong_total, steps, elapsed, enc_s, dec_s,
+                   box_enc, box_dec, ok, ranks_ok, gathered):
+    """The result dict of one uniform config from what run_uniform measured
+    (elapsed = max-over-ranks wall time of `steps` steps; enc_s / dec_s =
+    this rank's mean encode / decode launch): value, roofline (this rank's
+    launches, algorithmic bytes per SURVEY.md §8(d)), per-rank launch times
+    (a collective: every rank calls this), and on rank 0 the CPU baseline at
+    every world size.  Pure bookkeeping: tests/test_dist.py runs it at world
+    2 over gloo."""
+    ps = B // k + (1 if B % k else 0)
+    enc_bytes = S * (B + n * ps + 8 * n)
+    dec_bytes = S * (k * ps + B + k)
+    # user bytes of the whole job: weak = every rank's S; strong = the total
+    total_stripes = strong_total if strong_total else S * world
+    user_bytes = total_stripes * B * steps
+    dec = with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
+                    "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4), "us_per_launch": round(dec_s * 1e6, 2),
+                    "bytes_per_launch": dec_bytes}, box_dec)
+    res = {
+        "value": round(user_bytes / elapsed / 2**30, 3), "unit": "GiB/s", "steps": steps,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "timed_ms": round(elapsed * 1e3, 1),
+        "scaling": "strong" if strong_total else "weak",
+        "config": {"workload": desc, "n": n, "k": k, "block_size": B, "stripes_per_gpu": S, "part_size": ps,
+                   "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}",
+                   "stripes_all_gpus": total_stripes},
+        "roofline": with_box(roofline("nkfs_nk8_encode (encode + XXH64 per part)", enc_bytes, enc_s,
+                                      pmc_traffic(name, S, world)), box_enc),
+        "decode": dec,
+        "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
+        "per_rank": rank_spread(enc_s, dec_s, device),
+    }
+    if rank == 0 and not args.no_cpu:  # at every world size (rank 0's host cores)
+        res["cpu_baseline"] = cpu_baseline(S, B, n, k, args.cpu_seconds)
+    return res
+
+
 def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=0):
     """One uniform config: returns the result dict (value, roofline, ...).
     Weak scaling: `stripes` (default the config's) per GPU.  Strong scaling
     (strong_total > 0): that many stripes in all, split over the ranks."""
     import torch
     from nkfs_amd import batch, synth
-    S, B, n, k, desc = CONFIGS[name]
-    head = desc.split(", ")[0]  # "C3: N=8,K=5 encode(+XXH64/part)+decode(3 erased)"
-    if strong_total:
-        first, S = strong_range(rank, world, strong_total)
-        desc = (f"{head}, {strong_total} x {B // 1024} KiB stripes in all, split evenly over {world} GPU(s) "
-                f"(strong scaling; {S} on this GPU)")
-        world_bytes_scale = None
-    else:
-        if stripes:
-            S = stripes
-            desc = f"{head}, {S} x {B // 1024} KiB stripes per GPU"
-        first, _ = stripe_range(rank, S)
-        world_bytes_scale = world
+    _, B, n, k, _ = CONFIGS[name]
+    first, S, desc = workload(name, rank, world, stripes, strong_total)
     ps = batch.part_size(B, k)
     stream = torch.cuda.current_stream(device)
 
@@ -436,34 +480,13 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
             return [O.xxh64(p) for p in O.encode(synth.stripe_bytes(g, B), n, k, synth.stripe_ids(g, n))]
         ranks_ok = check_rank_digests(all_dig, n, expect)
     ok &= ranks_ok != -1
-    enc_bytes = S * (B + n * ps + 8 * n)
-    dec_bytes = S * (k * ps + B + k)
-    # user bytes of the whole job: weak = every rank's S; strong = the total
-    total_stripes = strong_total if strong_total else S * world_bytes_scale
-    user_bytes = total_stripes * B * steps
     # the box's own ceiling for each kernel's read:write mix, on the
     # kernel's own buffers (after verification: the probe overwrites them)
     hbm_anchor(blocks, parts, stream)
     box_enc = box_stream(blocks, parts, S * B, S * n * ps, stream)
     box_dec = box_stream(parts, out, S * k * ps, S * B, stream)
-    dec = with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
-                    "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4), "us_per_launch": round(dec_s * 1e6, 2),
-                    "bytes_per_launch": dec_bytes}, box_dec)
-    res = {
-        "value": round(user_bytes / elapsed / 2**30, 3), "unit": "GiB/s", "steps": steps,
-        "ms_per_step": round(elapsed / steps * 1e3, 4), "timed_ms": round(elapsed * 1e3, 1),
-        "scaling": "strong" if strong_total else "weak",
-        "config": {"workload": desc, "n": n, "k": k, "block_size": B, "stripes_per_gpu": S, "part_size": ps,
-                   "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}",
-                   "stripes_all_gpus": total_stripes},
-        "roofline": with_box(roofline("nkfs_nk8_encode (encode + XXH64 per part)", enc_bytes, enc_s,
-                                      pmc_traffic(name, S, world)), box_enc),
-        "decode": dec,
-        "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
-        "per_rank": rank_spread(enc_s, dec_s, device),
-    }
-    if rank == 0 and not args.no_cpu:  # at every world size (rank 0's host cores)
-        res["cpu_baseline"] = cpu_baseline(S, B, n, k, args.cpu_seconds)
+    res = uniform_result(name, args, rank, world, device, S, B, n, k, desc, strong_total, steps, elapsed, enc_s,
+                         dec_s, box_enc, box_dec, ok, ranks_ok, gathered)
     if rank == 0 and args.pcie:
         res["pcie_inclusive_GiBps"] = pcie_rate(batch, blocks, S, B, n, k, ids)
     del blocks, parts, out, digests
@@ -602,6 +625,30 @@ def reduce_sum(value: int, device) -> int:
     return int(t.item())
 
 
+def compose_line(args, rank, world, top, subs):
+    """The one JSON line (driver contract) from the headline result and the
+    sub-configs: metric, value, timing, the headline's roofline and CPU
+    baseline, the box's HBM anchor, the CPU model on rank 0."""
+    top = dict(top)
+    result = {
+        "metric": METRIC, "value": top.pop("value"), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": top.pop("ms_per_step"), "higher_is_better": True,
+        "scaling": top.pop("scaling"), "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846)",
+    }
+    top.pop("steps")
+    top.pop("unit")
+    result.update(top)
+    if subs:
+        result["configs"] = subs
+        result["verified"] = bool(result["verified"]) and all(v["verified"] for v in subs.values())
+    if _ANCHOR:
+        result["hbm_anchor"] = dict(_ANCHOR)
+    if rank == 0 and not args.no_cpu:
+        result["cpu_model"] = cpu_model()
+    return result
+
+
 def main():
     args = parse()
     import torch
@@ -634,22 +681,7 @@ def main():
             subs["c3s8"] = run("c3", None, CONFIGS["c3"][0] // 8)
         for name in ("c2", "c4", "c5", "w1", "w2"):
             subs[name] = run(name, None)
-    result = {
-        "metric": METRIC, "value": top.pop("value"), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": top.pop("ms_per_step"), "higher_is_better": True,
-        "scaling": top.pop("scaling"), "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (seeded splitmix64 stripes generated on device, seed 0x6E6B3846)",
-    }
-    top.pop("steps")
-    top.pop("unit")
-    result.update(top)
-    if subs:
-        result["configs"] = subs
-        result["verified"] = bool(result["verified"]) and all(v["verified"] for v in subs.values())
-    if _ANCHOR:
-        result["hbm_anchor"] = dict(_ANCHOR)
-    if rank == 0 and not args.no_cpu:
-        result["cpu_model"] = cpu_model()
+    result = compose_line(args, rank, world, top, subs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     import torch.distributed as dist

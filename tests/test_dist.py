@@ -136,3 +136,59 @@ def test_byte_balanced_ranges():
         assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
         per = [int(sizes[lo:hi].sum()) for lo, hi in ranges]
         assert max(per) - min(per) <= 2 * int(sizes.max())
+
+
+def _line_worker(rank, world, port, q):
+    """One rank of the bench line's bookkeeping at world 2 over gloo: the C3
+    strong-scaling workload, this rank's result from stand-in launch times
+    (no GPU here: the timings are test inputs, not measurements), the
+    per-rank spread collective, rank 0's CPU baseline and the composed line."""
+    import argparse
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    r, w, _ = bench.dist_setup("gloo")
+    dev = torch.device("cpu")
+    args = argparse.Namespace(no_cpu=False, cpu_seconds=0.02, steps=7, warmup=2)
+    first, S, desc = bench.workload("c3", r, w, 0, 8192)
+    _, B, n, k, _ = bench.CONFIGS["c3"]
+    enc_s, dec_s = 4.4e-3 * S / 8192 * (1 + 0.1 * r), 3.2e-3 * S / 8192
+    elapsed = bench.reduce_max(7 * (enc_s + dec_s), dev)
+    res = bench.uniform_result("c3", args, r, w, dev, S, B, n, k, desc, 8192, 7, elapsed, enc_s, dec_s, None, None,
+                               True, 2 if r == 0 else None, [1, 2])
+    line = bench.compose_line(args, r, w, res, {}) if r == 0 else None
+    q.put((r, first, S, desc, res["per_rank"], line))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_line_keys():
+    """the N > 1 line carries everything the N = 1 line
+    does -- roofline (achieved, frac, traffic key), decode roofline, the CPU
+    baseline and CPU model on rank 0 at world 2, per-rank encode / decode
+    times (max, min) -- and the strong-scaling label states the total split
+    over the GPUs, not a per-GPU batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_line_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=150) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (_, f0, s0, d0, pr0, line), (_, f1, s1, d1, pr1, _) = res
+    assert (f0, s0, f1, s1) == (0, 4096, 4096, 4096)
+    assert "8192 x 1024 KiB stripes in all, split evenly over 2 GPU(s)" in d0 and "per GPU" not in d0
+    assert pr0 == pr1 and len(pr0["encode_us"]) == 2
+    assert pr0["encode_us_max"] > pr0["encode_us_min"]
+    for key in ("metric", "value", "n_gpus", "ms_per_step", "roofline", "decode", "cpu_baseline", "cpu_model",
+                "per_rank", "config", "scaling"):
+        assert key in line, key
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    roof = line["roofline"]
+    assert {"achieved", "peak", "frac", "traffic", "bound", "unit"} <= set(roof)
+    assert roof["bytes_per_launch"] == 4096 * (1048576 + 8 * 209716 + 64)
+    cb = line["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["cores"] >= 1 and cb["value"] > 0
+    assert line["config"]["stripes_all_gpus"] == 8192
