@@ -57,6 +57,8 @@ namespace {
 
 
 
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
 constexpr int ENC_T = 16;                    // rows per lane per encode slice
 constexpr u32 ENC_ROWS = 256u * ENC_T;       // rows per encode workgroup
 
@@ -83,7 +85,7 @@ struct BigChain {
     u64 *digests;   // [stripe][n]
 };
 
-constexpr u64 CHAIN_TIMEOUT = 2000000;  // s_memrealtime ticks (100 MHz): 20 ms
+constexpr u64 CHAIN_TIMEOUT = 200000;  // s_memrealtime ticks (100 MHz): 2 ms (a slice takes ~35 us)
 
 template <bool HASH>
 __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *ids, const GfTables *gft,
@@ -92,7 +94,10 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];   // 16 tables of 256 x 16 B
     __shared__ __attribute__((aligned(16))) u32 stage[4 * 256];      // [part quad][row]
     __shared__ __attribute__((aligned(16))) uint4 coef[256];         // coef[m] = (x_{p0+e}^m), e < 16
-    __shared__ __attribute__((aligned(16))) u8 hx[HASH ? 16 * 256 : 16];  // [part][row] of a 256-row unit
+    // HASH: [part][row] copy of a 256-row unit for the XXH64 lanes, in
+    // coef's 4 KiB (coef is dead once the last chunk's tables are built):
+    // the LDS request stays at two workgroups per CU
+    u8 *const hx = reinterpret_cast<u8 *>(coef);
     __shared__ uint16_t glog[256];
     __shared__ u8 gexp[256];
 
@@ -245,22 +250,30 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     if (HASH && wave == 0) {
         hacc = xxh_acc_init(ha, 0);
         if (slice > 0) {
+            // the hand-off stays inside this XCD's L2: the producer (slice
+            // i-1) ran on the same XCD, its stores reached the L2 before its
+            // flag did, and these loads bypass the CU's L1 (sc0); an
+            // agent-scope release would write the whole L2 back per slice
+            const __amdgpu_buffer_rsrc_t fr = brsrc(ch.flag + unit, 4), xr = brsrc(ch.fail, 4);
             const u64 t0 = __builtin_amdgcn_s_memrealtime();
             u32 f;
             for (;;) {
-                f = __hip_atomic_load(ch.flag + unit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if (f >= slice || __hip_atomic_load(ch.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                f = __builtin_amdgcn_raw_buffer_load_b32(fr, 0, 0, 1);
+                if (f >= slice || __builtin_amdgcn_raw_buffer_load_b32(xr, 0, 0, 1))
                     break;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_TIMEOUT) {
                     if (lane == 0)
                         __hip_atomic_store(ch.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_s_sleep(2);
             }
             hok = f >= slice && f != 0xFFFFFFFFu;
-            if (hok)
-                hacc = ch.acc[u64(unit) * 64 + lane];
+            if (hok) {
+                const v2u w = __builtin_amdgcn_raw_buffer_load_b64(brsrc(ch.acc + u64(unit) * 64, 512),
+                                                                   u32(lane) * 8u, 0, 1);
+                hacc = (u64(w.y) << 32) | w.x;
+            }
         }
     }
 
@@ -326,13 +339,15 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     if constexpr (HASH) {
         if (wave == 0) {
             if (slice < last) {
-                // publish: the accumulators, then the flag (agent-scope
-                // release); a chain that could not be continued passes the
-                // failure on at once so no successor waits for it
+                // publish: the accumulators, then the flag (both land in
+                // this XCD's L2, in that order); a chain that could not be
+                // continued passes the failure on at once so no successor
+                // waits for it
                 ch.acc[u64(unit) * 64 + lane] = hacc;
+                __builtin_amdgcn_s_waitcnt(0);  // the accumulators are in the L2 before the flag
                 if (lane == 0)
                     __hip_atomic_store(ch.flag + unit, hok ? slice + 1 : 0xFFFFFFFFu, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
                 const int base = lane & ~3;
                 const u64 v1 = shfl64(hacc, base), v2 = shfl64(hacc, base + 1);

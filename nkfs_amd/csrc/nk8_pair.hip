@@ -153,12 +153,15 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
     __syncthreads();
 
     const bool oal = ((reinterpret_cast<uintptr_t>(out) | (g.block_sizes ? 0 : g.block_pitch)) & 15) == 0;
-    for (u32 r0 = rfirst; r0 < rend; r0 += RS) {
+    // the step loop runs on a wave-uniform row (the output stage needs every
+    // lane at its barrier and read-back, also lanes past the stripe's last row)
+    for (u32 rb = rfirst - 16 * lane; rb < rend; rb += RS) {
+        const u32 r0 = rb + 16 * lane;
         u32 o[U][8];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (u && r0 + u * R >= rend)
-                continue;
+            if (r0 + u * R >= rend)
+                continue;  // this lane's rows of the unit lie past the stripe (or its slice)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const u32 y = pa[u][q] ^ pb[u][q];
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const u32 ru = r0 - 16 * lane + u * R;  // first row of the unit
+            const u32 ru = rb + u * R;  // first row of the unit (wave-uniform)
             if (ru >= rend)
                 continue;  // wave-uniform
             if constexpr (XP) {

@@ -328,10 +328,20 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
         return -ENOSYS;
     int rc;
     // chunks of loads in flight per encoder wave (struct nkfs_tune.enc_ws_prefetch)
-    const int pf = nkfs_tune_now().enc_ws_prefetch;
+    // n > 4: struct nkfs_tune.enc_ws_waves overrides the caller's 4 encoder
+    // waves with 6 (three per stripe, 3,072-row chunks: the exchange then
+    // holds 99 KiB and the workgroup 7 waves, one per CU as before, with half
+    // as many loads again in flight)
+    const nkfs_tune t = nkfs_tune_now();
+    const int pf = t.enc_ws_prefetch;
+    if (g->n > 4 && ne == 4 && t.enc_ws_waves == 6)
+        ne = 6;
     if (g->n <= 4)
         rc = ne == 8 ? launch_ws<4, 8, false, 1>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<4, 4, false, 1>(g->k, st, *g, ids, digests, nt);
+    else if (ne == 6)
+        rc = pf >= 2 ? launch_ws<8, 6, false, 2>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<8, 6, false, 1>(g->k, st, *g, ids, digests, nt);
     else if (pf >= 2)
         rc = ne == 4 ? launch_ws<8, 4, false, 2>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<8, 2, false, 2>(g->k, st, *g, ids, digests, nt);
