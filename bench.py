@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time the host-memory (PCIe-inclusive) path")
     ap.add_argument("--stripes", type=int, default=0, help="override the stripes per GPU of a single --config")
+    ap.add_argument("--tune", default="", help="experiments only: struct nkfs_tune fields to set, k=v,k=v "
+                    "(recorded in the line; the default line uses the library's defaults)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="headline C3: strong = 8,192 stripes in all split over the GPUs (SURVEY.md §8(d)); "
                          "weak = 8,192 per GPU")
@@ -646,6 +648,8 @@ def compose_line(args, rank, world, top, subs):
         result["hbm_anchor"] = dict(_ANCHOR)
     if rank == 0 and not args.no_cpu:
         result["cpu_model"] = cpu_model()
+    if getattr(args, "tune", ""):
+        result["tune"] = args.tune
     return result
 
 
@@ -663,6 +667,12 @@ def main():
     from nkfs_amd import _lib
     L = _lib.lib()
     _lib.check(L.nkfs_gpu_init(local), "nkfs_gpu_init")
+    if args.tune:
+        t = _lib.get_tune()
+        for kv in args.tune.split(","):
+            key, val = kv.split("=")
+            setattr(t, key, int(val))
+        _lib.check(L.nkfs_tune_set(t), "nkfs_tune_set")
 
     head = HEADLINE if args.config == "all" else args.config
     strong = CONFIGS[HEADLINE][0] if (args.scaling == "strong" and head == HEADLINE and not args.stripes) else 0

@@ -35,7 +35,7 @@ class Tune(C.Structure):
     _fields_ = [(f, C.c_int) for f in ("enc_kernel", "dec_kernel", "enc_waves_per_cu", "dec_waves_per_cu",
                                        "dec_units", "enc_nib", "enc_units", "size_order", "enc_prefetch",
                                        "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units",
-                                       "enc_ws_prefetch", "enc_big_unfused", "dec_pair_stage",
+                                       "enc_ws_prefetch", "enc_big_fused", "dec_pair_stage",
                                        "host_depth", "host_lanes", "enc_ragged_split", "enc_ws_waves")]
 
 

@@ -235,20 +235,26 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             rows(std::false_type{});
     }
 
-    // XXH64 of the group's parts, fused (HASH): wave 0's lane 4e + a is
-    // accumulator a of part p0 + e.  The chain of a part is serial over all
-    // its rows, so slice i continues from the accumulators slice i-1's
-    // workgroup published (dispatched earlier on this XCD, normally long
-    // done); each 256-row unit is folded from an LDS [part][row] copy of its
-    // outputs while the unit is stored
-    const int he = lane >> 2, ha = lane & 3;
+    // XXH64 of the group's parts, fused (HASH): lane 4j + a < 16 of wave w
+    // is accumulator a of part p0 + 4w + j -- each wave hashes the four parts
+    // it transposes and stores, so a unit's fold needs no workgroup barrier
+    // and the four waves' serial rounds overlap.  The chain of a part is
+    // serial over all its rows, so slice i continues from the accumulators
+    // slice i-1's workgroup published (dispatched earlier on this XCD,
+    // normally long done); each 256-row unit is folded from the wave's LDS
+    // [part][row] copy of its outputs
+    __shared__ int chain_bad;
+    const int he = 4 * wave + (lane >> 2), ha = lane & 3;  // hash role of lanes < 16
+    const bool hl = lane < 16;
     const u32 unit = s * ngroups + grp;
     const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
     const u32 last = (v.ps - 1) / ENC_ROWS;
     u64 hacc = 0;
     bool hok = true;
-    if (HASH && wave == 0) {
+    if (HASH) {
         hacc = xxh_acc_init(ha, 0);
+        if (tid == 0)
+            chain_bad = 0;
         if (slice > 0) {
             // the hand-off stays inside this XCD's L2: the producer (slice
             // i-1) ran on the same XCD, its stores reached the L2 before its
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             hok = f >= slice && f != 0xFFFFFFFFu;
             if (hok) {
                 const v2u w = __builtin_amdgcn_raw_buffer_load_b64(brsrc(ch.acc + u64(unit) * 64, 512),
-                                                                   u32(lane) * 8u, 0, 1);
+                                                                   u32(16 * wave + (lane & 15)) * 8u, 0, 1);
                 hacc = (u64(w.y) << 32) | w.x;
             }
         }
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
         for (int j = 0; j < 4; ++j) {
             const int e = 4 * wave + j;
             if constexpr (HASH)
-                *reinterpret_cast<u32 *>(hx + e * 256 + 4 * lane) = o[j];
+                *reinterpret_cast<u32 *>(hx + e * 256 + 4 * lane) = o[j];  // this wave's own 1 KiB
             if (e < np && rr < v.ps) {
                 u8 *dst = v.parts + u64(p0 + e) * v.pitch + rr;
                 if (pal && rr + 4u <= v.ps) {
@@ -314,8 +320,10 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             }
         }
         if constexpr (HASH) {
-            __syncthreads();
-            if (wave == 0) {
+            // this wave's parts only: its LDS writes above are ordered before
+            // these reads (one wave), so no workgroup barrier is needed
+            __builtin_amdgcn_wave_barrier();
+            if (hl) {
                 // rounds of the 32-byte stripes that lie wholly below ps
                 const u8 *src = hx + he * 256 + 8 * ha;
                 const u32 s0 = rt >> 5;
@@ -334,29 +342,31 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                         tw[w] = tp[w];
                 }
             }
+            __builtin_amdgcn_wave_barrier();
         }
     }
     if constexpr (HASH) {
-        if (wave == 0) {
-            if (slice < last) {
-                // publish: the accumulators, then the flag (both land in
-                // this XCD's L2, in that order); a chain that could not be
-                // continued passes the failure on at once so no successor
-                // waits for it
-                ch.acc[u64(unit) * 64 + lane] = hacc;
-                __builtin_amdgcn_s_waitcnt(0);  // the accumulators are in the L2 before the flag
-                if (lane == 0)
-                    __hip_atomic_store(ch.flag + unit, hok ? slice + 1 : 0xFFFFFFFFu, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                const int base = lane & ~3;
-                const u64 v1 = shfl64(hacc, base), v2 = shfl64(hacc, base + 1);
-                const u64 v3 = shfl64(hacc, base + 2), v4 = shfl64(hacc, base + 3);
-                if (hok && ha == 0 && he < np) {
-                    u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
-                    h += v.ps;
-                    ch.digests[u64(s) * u64(n) + u64(p0 + he)] = xxh_tail_regs(h, tw, v.ps & 31);
-                }
+        if (slice < last) {
+            // publish: every wave's accumulators, then (after all of them
+            // reached this XCD's L2) the flag; a chain that could not be
+            // continued passes the failure on at once so no successor waits
+            if (hl)
+                ch.acc[u64(unit) * 64 + 16 * wave + lane] = hacc;
+            if (!hok)
+                chain_bad = 1;
+            __builtin_amdgcn_s_waitcnt(0);  // the accumulators are in the L2 before the flag
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(ch.flag + unit, chain_bad ? 0xFFFFFFFFu : slice + 1, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            const int base = lane & ~3;
+            const u64 v1 = shfl64(hacc, base), v2 = shfl64(hacc, base + 1);
+            const u64 v3 = shfl64(hacc, base + 2), v4 = shfl64(hacc, base + 3);
+            if (hok && hl && ha == 0 && he < np) {
+                u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+                h += v.ps;
+                ch.digests[u64(s) * u64(n) + u64(p0 + he)] = xxh_tail_regs(h, tw, v.ps & 31);
             }
         }
     }

@@ -757,13 +757,15 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
             return rc;
     }
     // else part groups of 8 for k <= 16 (then the batched XXH64 of the
-    // parts), 16-column chunks beyond (nk8_big.hip, XXH64 fused unless
-    // nkfs_tune.enc_big_unfused asks for the second pass)
+    // parts), 16-column chunks beyond (nk8_big.hip): XXH64 fused with
+    // nkfs_tune.enc_big_fused (HBM traffic 1.0x instead of 1.6x, but the
+    // chains' serial rounds in the store phase cost W2 ~6 %,
+    // profiles/r04/ab_w2_fused_*.txt), else a second pass (default)
     if (kern != NKFS_ENC_GENERIC) {
         rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
-        rc = digests && !nkfs_tune_now().enc_big_unfused ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
+        rc = digests && nkfs_tune_now().enc_big_fused ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
         if (rc != -ENOSYS)
             return rc;
         rc = nkfs_big_encode(g, ids, nullptr, gf, st);

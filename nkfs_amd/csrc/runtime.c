@@ -88,7 +88,7 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)) ||
 	    (t->dec_run_units != 1 && t->dec_run_units != 2 && t->dec_run_units != 4 && t->dec_run_units != 8 &&
 	     t->dec_run_units != 16) ||
-	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_unfused != 0 && t->enc_big_unfused != 1) ||
+	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_fused != 0 && t->enc_big_fused != 1) ||
 	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
 	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0 ||
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6))

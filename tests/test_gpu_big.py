@@ -68,10 +68,13 @@ def test_big_encode_matches(L, O, n, k, B, S):
         p0, d0 = batch.encode(blocks, B, n, k, ids)
     with _tuned(enc_kernel=_lib.ENC["big"]):
         p1, d1 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_lib.ENC["big"], enc_big_fused=1):  # XXH64 fused, chained over the slices
+        p3, d3 = batch.encode(blocks, B, n, k, ids)
     p2, d2 = batch.encode(blocks, B, n, k, ids)  # default dispatch
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
+    assert torch.equal(p0[:, :ps], p3[:, :ps]) and torch.equal(d0, d3)
     assert torch.equal(p0[:, :ps], p2[:, :ps]) and torch.equal(d0, d2)
     got = [u64(x) for x in d1.cpu().tolist()]
     for s in sorted({0, S - 1}):
@@ -99,16 +102,17 @@ def test_big_encode_ragged(L, O, n, k, gap):
         host[boff[s]: boff[s] + B] = synth.stripe_bytes(500 + s, int(B))
     ids_np = synth.batch_ids(len(sizes), n, first=500)
     outs = []
-    for kern in ("generic", "big"):
+    for kern, fused in (("generic", 0), ("big", 0), ("big", 1)):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-        with _tuned(enc_kernel=_lib.ENC[kern]):
+        with _tuned(enc_kernel=_lib.ENC[kern], enc_big_fused=fused):
             batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts,
                                 dev(poff), dig, int(sizes.max()))
         torch.cuda.synchronize()
         outs.append((parts.cpu().numpy(), [u64(x) for x in dig.cpu().tolist()]))
-    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
-    pn, got = outs[1]
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and outs[0][1] == o[1]
+    pn, got = outs[2]
     for s in (0, 2, 3, 4, len(sizes) - 1):
         B = int(sizes[s])
         want = O.encode(host[boff[s]: boff[s] + B], n, k, ids_np[s])
@@ -170,18 +174,18 @@ def test_big_decode_matches(L, O, n, k, B, S):
 
 
 def test_big_round_trip_w2(L, O):
-    """The bench's W2 batch (256 x 1 MiB, N48K32): default encode (XXH64
-    fused, each slice continuing its part group's chains from the previous
-    slice's workgroup) gives the same parts and digests as the encoder with
-    the separate hash pass, the oracle's digests on a sample; keep 32 seeded
-    survivors -> default decode gives every block back."""
+    """The bench's W2 batch (256 x 1 MiB, N48K32): the encoder with XXH64
+    fused (each slice continuing its part group's chains from the previous
+    slice's workgroup) gives the same parts and digests as the default one
+    with the separate hash pass, the oracle's digests on a sample; keep 32
+    seeded survivors -> default decode gives every block back."""
     from nkfs_amd import _lib, batch
     S, B, n, k = 256, 1048576, 48, 32
     blocks = batch.synth(S, B, first=11)
     ids_np = synth.batch_ids(S, n, first=11)
     ids = dev(ids_np)
     parts, dig = batch.encode(blocks, B, n, k, ids)
-    with _tuned(enc_big_unfused=1):
+    with _tuned(enc_big_fused=1 - _lib.get_tune().enc_big_fused):
         parts1, dig1 = batch.encode(blocks, B, n, k, ids)
     torch.cuda.synchronize()
     assert torch.equal(parts, parts1) and torch.equal(dig, dig1)
