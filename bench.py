@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time the host-memory (PCIe-inclusive) path")
     ap.add_argument("--stripes", type=int, default=0, help="override the stripes per GPU of a single --config")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="control collectives: nccl (RCCL over xGMI, the real run) or gloo (CPU; rehearses the "
+                         "multi-rank path with ranks sharing GPUs, e.g. 2 ranks on a 1-GPU box -- not a measurement)")
     ap.add_argument("--tune", default="", help="experiments only: struct nkfs_tune fields to set, k=v,k=v "
                     "(recorded in the line; the default line uses the library's defaults)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
@@ -124,13 +127,22 @@ def byte_balanced_ranges(sizes, world: int):
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+_CDEV = None  # collectives' device when it differs from the data's (--backend gloo: the CPU)
+
+
+def cdev(device):
+    """Device the control collectives run on: the rank's GPU under RCCL
+    (backend nccl), the CPU under gloo (a rehearsal of the multi-rank path)."""
+    return _CDEV if _CDEV is not None else device
+
+
 def rank_spread(enc_s: float, dec_s: float, device) -> dict:
     """Every rank's mean encode / decode launch time (µs), all-gathered, so
     that a line at N > 1 shows the imbalance between ranks (max and min next
     to the per-rank list; the headline's roofline is rank 0's launches)."""
     import torch
     import torch.distributed as dist
-    v = torch.tensor([enc_s * 1e6, dec_s * 1e6], dtype=torch.float64, device=device)
+    v = torch.tensor([enc_s * 1e6, dec_s * 1e6], dtype=torch.float64, device=cdev(device))
     if dist.is_available() and dist.is_initialized():
         out = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
         dist.all_gather(out, v)
@@ -147,7 +159,7 @@ def reduce_max(value: float, device) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=cdev(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -158,7 +170,7 @@ def gather_digest_xor(local_xor: int, device) -> list[int]:
     import torch
     import torch.distributed as dist
     v = torch.tensor([local_xor - (1 << 64) if local_xor >= (1 << 63) else local_xor], dtype=torch.int64,
-                     device=device)
+                     device=cdev(device))
     if not (dist.is_available() and dist.is_initialized()):
         return [local_xor]
     out = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
@@ -175,6 +187,7 @@ def gather_digests(local, device):
     if not (dist.is_available() and dist.is_initialized()):
         return [local.cpu()]
     world = dist.get_world_size()
+    device = cdev(device)
     cnt = torch.tensor([local.numel()], dtype=torch.int64, device=device)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(cnts, cnt)
@@ -622,7 +635,7 @@ def reduce_sum(value: int, device) -> int:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return value
-    t = torch.tensor([value], dtype=torch.int64, device=device)
+    t = torch.tensor([value], dtype=torch.int64, device=cdev(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
 
@@ -650,6 +663,8 @@ def compose_line(args, rank, world, top, subs):
         result["cpu_model"] = cpu_model()
     if getattr(args, "tune", ""):
         result["tune"] = args.tune
+    if getattr(args, "backend", "nccl") != "nccl":
+        result["backend"] = f"{args.backend} (rehearsal: ranks may share a GPU; not a measurement)"
     return result
 
 
@@ -659,10 +674,16 @@ def main():
 
     # the rank's GPU is selected before the process group exists, so RCCL's
     # communicator binds to it (one process per GPU)
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    rank, world, local = dist_setup("nccl")
-    device = torch.device("cuda", local)
-    os.environ["NKFS_DEVICE"] = str(local)
+    global _CDEV
+    ngpu = max(1, torch.cuda.device_count())
+    gpu = int(os.environ.get("LOCAL_RANK", "0")) % ngpu  # gloo rehearsal: ranks may share a GPU
+    torch.cuda.set_device(gpu)
+    rank, world, local = dist_setup(args.backend)
+    if args.backend == "gloo":
+        _CDEV = torch.device("cpu")
+    device = torch.device("cuda", gpu)
+    os.environ["NKFS_DEVICE"] = str(gpu)
+    local = gpu
 
     from nkfs_amd import _lib
     L = _lib.lib()

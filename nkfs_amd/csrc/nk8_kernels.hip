@@ -656,7 +656,7 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids,
                                  void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                  hipStream_t st);
 extern "C" int nkfs_pair_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *gf, int xp, hipStream_t st);
+                                int navail, int32_t *status, const void *gf, int xp, int waves, hipStream_t st);
 extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                hipStream_t st);
@@ -827,7 +827,8 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
                                                                  : NKFS_DEC_SLICE;
         if (kern == NKFS_DEC_PAIR && !expect) {
             auto pair = [&](const nkfs_geom *go) {
-                return nkfs_pair_decode(go, n_slots, ids, avail, navail, status, gf, t.dec_pair_stage, st);
+                return nkfs_pair_decode(go, n_slots, ids, avail, navail, status, gf, t.dec_pair_stage,
+                                        t.dec_pair_waves, st);
             };
             rc = with_size_order(g, st, pair);
             if (rc == -ENOSYS)

@@ -47,16 +47,25 @@ __device__ inline u32 gfm_bits(u32 a, u32 b)
 
 constexpr int R = 1024;  // rows per unit: 16 per lane
 
-template <int U, bool XP>
-__global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
-                                                    int navail, int32_t *status, const GfTables *gft, u32 slices)
+// WPB waves per workgroup, each an independent (stripe, slice) with its own
+// LDS: only wave-level ordering inside (no workgroup barrier), so a wave
+// that finds its stripe out of range or undecodable simply leaves.  WPB = 4
+// quarters the workgroups the dispatcher launches for 4 KiB stripes.
+template <int U, bool XP, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_decode_pair(nkfs_geom g, int n_slots, const u8 *ids,
+                                                          const u8 *avail, int navail, int32_t *status,
+                                                          const GfTables *gft, u32 slices)
 {
     constexpr int RS = R * U;  // rows per step
-    __shared__ __attribute__((aligned(16))) u32 tbl[256];
-    __shared__ __attribute__((aligned(16))) u8 stage[XP ? 2 * R : 16];
-    __shared__ __attribute__((aligned(4))) u8 inv_s[256];
-    const int lane = threadIdx.x;
-    const u32 s = blockIdx.x / slices, slice = blockIdx.x % slices;
+    __shared__ __attribute__((aligned(16))) u32 tbl_all[WPB][256];
+    __shared__ __attribute__((aligned(16))) u8 stage_all[WPB][XP ? 2 * R : 16];
+    __shared__ __attribute__((aligned(4))) u8 inv_all[WPB][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u32 *const tbl = tbl_all[wave];
+    u8 *const stage = stage_all[wave];
+    u8 *const inv_s = inv_all[wave];
+    const u32 vw = blockIdx.x * WPB + wave;  // this wave's (stripe, slice)
+    const u32 s = vw / slices, slice = vw % slices;
     if (s >= g.nstripes)
         return;
     const u32 sl = g.order ? g.order[s] : s;
@@ -142,7 +151,7 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
     }
     if (lane == 0 && status && slice == 0)
         status[sl] = 0;
-    __syncthreads();  // inv_s
+    __builtin_amdgcn_wave_barrier();  // inv_s (this wave's LDS: in order within the wave)
     // T[y] = (x_a c y) | (c y) << 8, c = 1 / (x_a ^ x_b): linear in y, so
     // eight basis products and a Gray-code walk fill it (build_table)
     const u32 c = inv_s[x0 ^ x1];
@@ -150,7 +159,7 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
     u32 basis[8][1];
     make_basis<1>(basis, row);
     build_table<1, 64>(reinterpret_cast<u8 *>(tbl), basis, lane);
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
 
     const bool oal = ((reinterpret_cast<uintptr_t>(out) | (g.block_sizes ? 0 : g.block_pitch)) & 15) == 0;
     // the step loop runs on a wave-uniform row (the output stage needs every
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
                 // 1024 + 16l of the unit: one contiguous 1 KiB per instruction
                 *reinterpret_cast<uint4 *>(stage + 32 * lane) = make_uint4(o[u][0], o[u][1], o[u][2], o[u][3]);
                 *reinterpret_cast<uint4 *>(stage + 32 * lane + 16) = make_uint4(o[u][4], o[u][5], o[u][6], o[u][7]);
-                __syncthreads();
+                __builtin_amdgcn_wave_barrier();
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const uint4 t = *reinterpret_cast<const uint4 *>(stage + 1024 * h + 16 * lane);
@@ -204,7 +213,7 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
                             out[off + b] = u8(tw[b >> 2] >> (8 * (b & 3)));
                     }
                 }
-                __syncthreads();
+                __builtin_amdgcn_wave_barrier();
             } else {
                 const u32 rl = ru + 16 * lane;
                 if (rl >= rend)
@@ -227,9 +236,10 @@ __global__ __launch_bounds__(64) void k_decode_pair(nkfs_geom g, int n_slots, co
 
 // k = 2 decode of a uniform or ragged batch (g->order honoured), no
 // integrity check (the verifying form stays on the wave decoder).  xp: stage
-// the output through LDS.  -ENOSYS outside k = 2.
+// the output through LDS; waves: waves per workgroup (1 or 4).  -ENOSYS
+// outside k = 2.
 extern "C" int nkfs_pair_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *gf, int xp, hipStream_t st)
+                                int navail, int32_t *status, const void *gf, int xp, int waves, hipStream_t st)
 {
     if (g->k != 2 || navail < 2 || (!g->block_sizes && (g->part_pitch & 15)))
         return -ENOSYS;
@@ -246,11 +256,22 @@ extern "C" int nkfs_pair_decode(const nkfs_geom *g, int n_slots, const uint8_t *
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
     const GfTables *t = static_cast<const GfTables *>(gf);
-    if (xp)
-        hipLaunchKernelGGL((k_decode_pair<U, true>), dim3(u32(grid)), dim3(64), 0, st, *g, n_slots, ids, avail,
-                           navail, status, t, slices);
-    else
-        hipLaunchKernelGGL((k_decode_pair<U, false>), dim3(u32(grid)), dim3(64), 0, st, *g, n_slots, ids, avail,
-                           navail, status, t, slices);
+    // one wave per workgroup, or four (waves 1..3 of the last workgroup may
+    // find no stripe and leave)
+    const u32 wpb = waves >= 4 ? 4 : 1;
+    const dim3 gd(u32((grid + wpb - 1) / wpb)), bd(64 * wpb);
+#define NKFS_PAIR(XX, WW) \
+    hipLaunchKernelGGL((k_decode_pair<U, XX, WW>), gd, bd, 0, st, *g, n_slots, ids, avail, navail, status, t, slices)
+    if (wpb == 4) {
+        if (xp)
+            NKFS_PAIR(true, 4);
+        else
+            NKFS_PAIR(false, 4);
+    } else if (xp) {
+        NKFS_PAIR(true, 1);
+    } else {
+        NKFS_PAIR(false, 1);
+    }
+#undef NKFS_PAIR
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

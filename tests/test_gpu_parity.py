@@ -937,8 +937,8 @@ def test_pair_decode_matches(L, O, n, B, S):
         ids2[1, av[1, 1]] = ids2[1, av[1, 0]]
         ids2[2, :] = ids2[2, 0]
     outs = []
-    for kern, stage in (("wave", 1), ("pair", 1), ("pair", 0)):
-        with _tuned(dec_kernel=_dec(kern), dec_pair_stage=stage):
+    for kern, stage, waves in (("wave", 1, 4), ("pair", 1, 4), ("pair", 0, 1), ("pair", 1, 1), ("pair", 0, 4)):
+        with _tuned(dec_kernel=_dec(kern), dec_pair_stage=stage, dec_pair_waves=waves):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
             torch.cuda.synchronize()
@@ -960,8 +960,8 @@ def test_pair_decode_matches(L, O, n, B, S):
     assert np.array_equal(np.asarray(O.decode([pn[j] for j in sel], ids_np[s][sel], k, B)), blocks[s, :B].cpu().numpy())
 
 
-@pytest.mark.parametrize("gap,stage", [(0, 1), (3, 1), (5, 0)])
-def test_pair_decode_ragged(L, gap, stage):
+@pytest.mark.parametrize("gap,stage,waves", [(0, 1, 4), (3, 1, 1), (5, 0, 4), (0, 0, 1)])
+def test_pair_decode_ragged(L, gap, stage, waves):
     """The k = 2 decoder on a ragged batch (size order applied, blocks at
     unaligned offsets): every stripe back bit-exact, gap bytes untouched."""
     from nkfs_amd import batch
@@ -978,7 +978,7 @@ def test_pair_decode_ragged(L, gap, stage):
                         None, int(sizes.max()))
     avail = synth.batch_survivors(len(sizes), n, 3, first=700)
     out = torch.zeros(pos + 16, dtype=torch.uint8, device="cuda")
-    with _tuned(dec_kernel=_dec("pair"), dec_pair_stage=stage):
+    with _tuned(dec_kernel=_dec("pair"), dec_pair_stage=stage, dec_pair_waves=waves):
         status = batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(avail), k, out, dev(boff),
                                      dev(sizes.astype(np.int32)), int(sizes.max()))
     torch.cuda.synchronize()
