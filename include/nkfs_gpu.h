@@ -93,6 +93,8 @@ struct nkfs_tune {
 	int enc_ragged_split; /* ragged n > 4 encode: parts >= this many bytes on the warp-specialised kernel (0 = all walk) */
 	int enc_ws_waves;     /* warp-specialised encoder, n > 4: encoder waves per workgroup (4 default, or 6) */
 	int dec_pair_waves;   /* k = 2 decoder: waves (one stripe each) per workgroup (1 or 4) */
+	int enc_few_max;      /* n <= 8 encode of at most this many big stripes (< 16 MiB of parts): the row-parallel
+	                         general kernels + a hash pass instead of one wave per stripe (0..63) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

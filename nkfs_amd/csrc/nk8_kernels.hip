@@ -726,8 +726,9 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
 static bool few_big_stripes(const nkfs_geom *g)
 {
     const u32 ps = max_part_size(g, g->block_size);
-    return !g->block_sizes && nkfs_tune_now().enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
-           g->nstripes < 64 && ps >= 1024;
+    const nkfs_tune t = nkfs_tune_now();
+    return !g->block_sizes && t.enc_kernel == NKFS_ENC_AUTO && u64(g->nstripes) * ps < (u64(16) << 20) &&
+           g->nstripes <= u32(t.enc_few_max) && ps >= 1024;
 }
 
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,

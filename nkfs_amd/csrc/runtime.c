@@ -65,6 +65,7 @@ static struct nkfs_tune g_tune = {
 	.host_depth = 6,  /* C3 1 GiB PUT / GET: 17.2 / 27.6 GiB/s at 3 x 1, 21.5 / 34.1 at 6 x 2 */
 	.host_lanes = 2,  /* (profiles/r04/pcie.txt) */
 	.enc_ws_waves = 4,
+	.enc_few_max = 63,
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
 
@@ -92,7 +93,8 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_fused != 0 && t->enc_big_fused != 1) ||
 	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
 	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0 ||
-	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4))
+	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||
+	    t->enc_few_max < 0 || t->enc_few_max > 63)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;
