@@ -95,6 +95,8 @@ struct nkfs_tune {
 	int dec_pair_waves;   /* k = 2 decoder: waves (one stripe each) per workgroup (1 or 4) */
 	int enc_few_max;      /* n <= 8 encode of at most this many big stripes (< 16 MiB of parts): the row-parallel
 	                         general kernels + a hash pass instead of one wave per stripe (0..63) */
+	int enc_ws_hash_waves; /* warp-specialised encoder, n > 4 with 4 encoder waves: hash waves per workgroup
+	                          (0 auto: 2 from 1,024 stripes on; 1; 2) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

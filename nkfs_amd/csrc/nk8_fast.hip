@@ -418,8 +418,13 @@ __device__ inline u32 gfm(u32 a, u32 b)
 
 // U = 16-row units per lane per step (one-shot steps for short stripes: a
 // 4 KiB N4K2 stripe is a single step of 2 x 1024 rows at U = 2)
+// NKFS_DEC_FAST_WPE: waves per SIMD requested for the non-verifying form
+// (0: the compiler's choice -- 102 SGPRs, 7 waves per SIMD for k = 2)
+#ifndef NKFS_DEC_FAST_WPE
+#define NKFS_DEC_FAST_WPE 0
+#endif
 template <int K, int E, int G, int U, bool VERIFY>
-__global__ __launch_bounds__(64) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VERIFY || !NKFS_DEC_FAST_WPE ? 1 : NKFS_DEC_FAST_WPE))) void k_decode_fast(nkfs_geom g, int n_slots, const u8 *ids, const u8 *avail,
                                                     int navail, int32_t *status, const u8 *inv, bool nt, int slices,
                                                     const u64 *expect, u64 *badmask)
 {

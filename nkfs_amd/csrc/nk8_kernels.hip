@@ -677,10 +677,17 @@ static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
     // 3,045 GB/s; 65,536 x 4 KiB walk 3,027 / fused 2,669; 2,048 x 256 KiB
     // walk 4,373 / ws 4,263; 256 x 64 KiB ws 1,552 / walk 1,111; 16,384 x
     // 512 KiB ws 4,964 / walk 4,881.
+    // Round 4: with two hash waves per workgroup (>= 1,024 stripes) the
+    // warp-specialised kernel also wins from 48 KiB parts: 16,384 x 256 KiB
+    // ws2 4,960 / walk 4,901, 2,048 x 256 KiB 4,650 / 4,549; 131,072-byte
+    // blocks (26 KiB parts) stay on the walk encoder, 4,764 / 4,875
+    // (profiles/r04/seam_ws2.txt).
     if (g->block_sizes || !digests || g->n <= 4)
         return 0;
     const u32 ps = (g->block_size + u32(g->k) - 1) / u32(g->k);
-    const bool ws = ps >= 65536 || (ps >= 32768 && g->nstripes <= 1024) || (ps >= 8192 && g->nstripes <= 256);
+    const bool ws2 = g->nstripes >= 1024 && nkfs_tune_now().enc_ws_hash_waves != 1;
+    const bool ws = ps >= 65536 || (ps >= 32768 && g->nstripes <= 1024) || (ps >= 8192 && g->nstripes <= 256) ||
+                    (ws2 && ps >= 49152);
     return !ws;
 }
 

@@ -18,6 +18,12 @@
 //   * encoded parts go to HBM and to a double-buffered LDS exchange;
 //   * the hash wave (lane = stripe, part, accumulator) folds chunk c-1 from
 //     LDS while the encoders produce chunk c; one barrier per chunk.
+// HW = 2 hash waves own S = 2 * 16 / E stripes (n > 4: four stripes of 1,024
+// rows per chunk instead of two of 2,048).  One XXH64 round is ~35 ns of
+// dependent 64-bit multiplies, so a hash wave folds at most ~14.5 GB/s:
+// with one per CU that is ~3.7 TB/s of parts, i.e. a ~6 TB/s ceiling on the
+// N8K5 encode (61 % of its bytes are hashed) that a fast box's HBM reaches
+// (tools/xxh_rate.hip).
 // Packed product tables T_m[x] = (ids_0^m * x, ..., ids_{n-1}^m * x),
 // m = 1..k-1, are built per stripe in LDS exactly as in k_encode_fast.
 #include <hip/hip_runtime.h>
@@ -34,10 +40,11 @@ using namespace nkfs::dev;
 
 // SB: single-buffered exchange (the hash wave copies its words to registers
 // between two barriers per chunk) -- half the LDS, so more workgroups per CU
-template <int K, int E, int NE, bool SB, int PF>
-__global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
+template <int K, int E, int NE, bool SB, int PF, int HW>
+__global__ __launch_bounds__(64 * (NE + HW)) void k_encode_ws(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
-    constexpr int S = 16 / E;       // stripes per workgroup: 4 accumulators x E parts x S = 64 chains
+    constexpr int SPH = 16 / E;     // stripes per hash wave: 4 accumulators x E parts x SPH = 64 chains
+    constexpr int S = HW * SPH;     // stripes per workgroup
     constexpr int WPS = NE / S;     // encoder waves per stripe
     static_assert(NE % S == 0 && WPS >= 1, "encoder waves per stripe");
     constexpr int CR = WPS * 1024;  // rows per stripe per chunk
@@ -49,7 +56,7 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     __shared__ __attribute__((aligned(16))) u8 xbuf[SB ? 1 : 2][S * E * SP];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const bool hasher = wave == NE;
+    const bool hasher = wave >= NE;
     const int n = g.n;
 
     // chunks the workgroup iterates: the largest of its stripes' (ragged)
@@ -212,8 +219,8 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     }
 
     // ------------------------------------------------------------ hash wave
-    constexpr int LPS = 64 / S;  // hash lanes per stripe (4 x E)
-    const int hs = lane / LPS, hli = lane % LPS;
+    constexpr int LPS = 64 / SPH;  // hash lanes per stripe (4 x E)
+    const int hs = (wave - NE) * SPH + lane / LPS, hli = lane % LPS;
     const int hi = hli >> 2, ha = hli & 3;
     u32 s;
     const bool live = slot_live(g, blockIdx.x * S + hs, s);
@@ -295,15 +302,15 @@ __global__ __launch_bounds__(64 * (NE + 1)) void k_encode_ws(nkfs_geom g, const 
     }
 }
 
-template <int E, int NE, bool SB, int PF>
+template <int E, int NE, bool SB, int PF, int HW = 1>
 static int launch_ws(int k, hipStream_t st, const nkfs_geom &g, const uint8_t *ids, uint64_t *dig, bool nt)
 {
-    constexpr int S = 16 / E;
-    const dim3 grid((g.nstripes + S - 1) / S), block(64 * (NE + 1));
+    constexpr int S = HW * 16 / E;
+    const dim3 grid((g.nstripes + S - 1) / S), block(64 * (NE + HW));
     switch (k) {
 #define NKFS_K(KK)                                                                         \
     case KK:                                                                               \
-        hipLaunchKernelGGL((k_encode_ws<KK, E, NE, SB, PF>), grid, block, 0, st, g, ids, dig, nt); \
+        hipLaunchKernelGGL((k_encode_ws<KK, E, NE, SB, PF, HW>), grid, block, 0, st, g, ids, dig, nt); \
         return 0;
         NKFS_K(2)
         NKFS_K(3)
@@ -328,6 +335,10 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
         return -ENOSYS;
     int rc;
     // chunks of loads in flight per encoder wave (struct nkfs_tune.enc_ws_prefetch)
+    // n > 4: struct nkfs_tune.enc_ws_hash_waves picks one or two hash waves
+    // per workgroup (0: two from 1,024 stripes on, where the grid of four-
+    // stripe workgroups still fills the chip: N8K5 1,024-16,384 x 512 KiB
+    // +1-4 %, 16,384 x 256 KiB +1-6 %, 256 stripes -30 %; seam_ws2.txt);
     // n > 4: struct nkfs_tune.enc_ws_waves overrides the caller's 4 encoder
     // waves with 6 (three per stripe, 3,072-row chunks: the exchange then
     // holds 99 KiB and the workgroup 7 waves, one per CU as before, with half
@@ -339,6 +350,9 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
     if (g->n <= 4)
         rc = ne == 8 ? launch_ws<4, 8, false, 1>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<4, 4, false, 1>(g->k, st, *g, ids, digests, nt);
+    else if (ne == 4 && (t.enc_ws_hash_waves == 2 || (!t.enc_ws_hash_waves && g->nstripes >= 1024)))
+        rc = pf >= 2 ? launch_ws<8, 4, false, 2, 2>(g->k, st, *g, ids, digests, nt)
+                     : launch_ws<8, 4, false, 1, 2>(g->k, st, *g, ids, digests, nt);
     else if (ne == 6)
         rc = pf >= 2 ? launch_ws<8, 6, false, 2>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<8, 6, false, 1>(g->k, st, *g, ids, digests, nt);

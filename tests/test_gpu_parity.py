@@ -506,25 +506,26 @@ def _dec(name):
     return _lib.DEC[name]
 
 
-@pytest.mark.parametrize("n,k,B", [(4, 2, 4096), (4, 3, 70001), (8, 5, 262144), (8, 6, 1000)])
-def test_warp_specialised_encode_matches(L, n, k, B):
-    """The warp-specialised encoder (nk8_ws.hip: encoder waves + one hash
-    wave per workgroup; chosen by the shape rules for grids of <= 2 waves
-    per SIMD of big stripes, forced here through struct nkfs_tune) writes the
-    same parts and digests as the fused kernel, tails and partial
-    workgroups included."""
+@pytest.mark.parametrize("n,k,B,hw", [(4, 2, 4096, 1), (4, 3, 70001, 1), (8, 5, 262144, 1), (8, 6, 1000, 1),
+                                      (8, 5, 262144, 2), (8, 6, 1000, 2), (5, 2, 70001, 2), (8, 8, 3, 2)])
+def test_warp_specialised_encode_matches(L, n, k, B, hw):
+    """The warp-specialised encoder (nk8_ws.hip: encoder waves + one or two
+    hash waves per workgroup; chosen by the shape rules for grids of <= 2
+    waves per SIMD of big stripes, forced here through struct nkfs_tune)
+    writes the same parts and digests as the fused kernel, tails and partial
+    workgroups (23 stripes: 5 workgroups of 4 + 3) included."""
     from nkfs_amd import batch
-    S = 23
-    blocks = batch.synth(S, B, first=77)
-    ids = dev(synth.batch_ids(S, n, first=77))
-    with _tuned(enc_kernel=_enc("fused")):
-        p0, d0 = batch.encode(blocks, B, n, k, ids)
-    with _tuned(enc_kernel=_enc("ws")):
-        p1, d1 = batch.encode(blocks, B, n, k, ids)
-    torch.cuda.synchronize()
-    ps = batch.part_size(B, k)
-    assert torch.equal(p0[:, :ps], p1[:, :ps])
-    assert torch.equal(d0, d1)
+    for S in (23, 2, 1):
+        blocks = batch.synth(S, B, first=77)
+        ids = dev(synth.batch_ids(S, n, first=77))
+        with _tuned(enc_kernel=_enc("fused")):
+            p0, d0 = batch.encode(blocks, B, n, k, ids)
+        with _tuned(enc_kernel=_enc("ws"), enc_ws_hash_waves=hw):
+            p1, d1 = batch.encode(blocks, B, n, k, ids)
+        torch.cuda.synchronize()
+        ps = batch.part_size(B, k)
+        assert torch.equal(p0[:, :ps], p1[:, :ps]), S
+        assert torch.equal(d0, d1), S
 
 
 @pytest.mark.parametrize("S,B", [(2200, 163840), (3500, 131072), (1700, 1048576)])
@@ -724,8 +725,8 @@ def test_ragged_kernels_match(L, O, n, k, gap, order):
         hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(1300 + s_, int(Bs))
     rid = synth.batch_ids(len(sizes), n, first=1300)
     outs = []
-    for kern in ("walk", "fused", "ws"):
-        with _tuned(enc_kernel=_enc(kern), size_order=order):
+    for kern, hw in (("walk", 1), ("fused", 1), ("ws", 1), ("ws", 2)):
+        with _tuned(enc_kernel=_enc(kern), size_order=order, enc_ws_hash_waves=hw):
             parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
             dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
             batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff),
@@ -826,7 +827,7 @@ def test_ragged_slice_decode_past_2gib(L, n, k, units):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("S,B", [(512, 1048576), (1024, 1048576), (512, 262144)])
+@pytest.mark.parametrize("S,B", [(512, 1048576), (1024, 1048576), (512, 262144), (1024, 262144)])
 def test_bench_kernels_against_oracle(L, O, S, B):
     """The kernels the bench times, pinned through struct nkfs_tune and
     compared with the oracle directly (not only with another kernel): the
@@ -841,8 +842,9 @@ def test_bench_kernels_against_oracle(L, O, S, B):
     ids = dev(ids_np)
     ps = batch.part_size(B, k)
     sample = sorted({int(x) for x in np.linspace(0, S - 1, 16)})
-    for kern, pf, ne in (("ws", 1, 4), ("ws", 2, 4), ("ws", 1, 6), ("ws", 2, 6), ("walk", 1, 4)):
-        with _tuned(enc_kernel=_enc(kern), enc_ws_prefetch=pf, enc_ws_waves=ne):
+    for kern, pf, ne, hw in (("ws", 1, 4, 1), ("ws", 2, 4, 1), ("ws", 1, 6, 1), ("ws", 2, 6, 1), ("ws", 1, 4, 2),
+                             ("ws", 2, 4, 2), ("walk", 1, 4, 1), ("auto", 1, 4, 0)):
+        with _tuned(enc_kernel=_enc(kern), enc_ws_prefetch=pf, enc_ws_waves=ne, enc_ws_hash_waves=hw):
             parts, dig = batch.encode(blocks, B, n, k, ids)
         torch.cuda.synchronize()
         got = [u64(x) for x in dig.cpu().tolist()]

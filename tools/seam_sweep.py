@@ -21,8 +21,14 @@ import torch  # noqa: E402
 from kbench import timeit  # noqa: E402
 from nkfs_amd import _lib, batch, synth  # noqa: E402
 
-ENC = {"auto": {}, "walk": {"enc_kernel": 1}, "fused": {"enc_kernel": 2}, "ws": {"enc_kernel": 3}}
+ENC = {"auto": {}, "walk": {"enc_kernel": 1}, "fused": {"enc_kernel": 2}, "ws": {"enc_kernel": 3},
+       "ws2": {"enc_kernel": 3, "enc_ws_hash_waves": 2}}
 DEC = {"auto": {}, "slice": {"dec_kernel": 1}, "wave": {"dec_kernel": 2}}
+# SWEEP_ENC=auto,walk,ws2 / SWEEP_DEC= (none) / SWEEP_SHAPES=n8 (N8K5 64 KiB-1 MiB only) narrow a run
+if os.environ.get("SWEEP_ENC"):
+    ENC = {e: ENC[e] for e in os.environ["SWEEP_ENC"].split(",")}
+if "SWEEP_DEC" in os.environ:
+    DEC = {d: DEC[d] for d in filter(None, os.environ["SWEEP_DEC"].split(","))}
 
 
 def main():
@@ -31,8 +37,9 @@ def main():
     _lib.check(L.nkfs_gpu_init(0))
     shapes = [(8, 5, B, S) for B in (65536, 131072, 262144, 524288, 1048576)
               for S in ((256, 1024, 2048, 4096, 8192, 16384) if not quick else (1024, 4096))]
-    shapes += [(4, 2, B, S) for B in (4096, 16384, 65536, 262144) for S in (1024, 8192, 65536)]
-    shapes += [(8, 5, B, S) for B in (4096, 20480) for S in (1024, 8192, 65536)]
+    if os.environ.get("SWEEP_SHAPES") != "n8":
+        shapes += [(4, 2, B, S) for B in (4096, 16384, 65536, 262144) for S in (1024, 8192, 65536)]
+        shapes += [(8, 5, B, S) for B in (4096, 20480) for S in (1024, 8192, 65536)]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "3"))
     print(f"{'n':>2} {'k':>2} {'S':>6} {'B':>8} {'ps':>7} {'fused_waves':>11} | encode GB/s: " + " ".join(f"{e:>6}" for e in ENC)
           + " | decode GB/s: " + " ".join(f"{d:>6}" for d in DEC), flush=True)
@@ -80,6 +87,8 @@ def main():
                         dr[name].append(dec_b / timeit(dec, reps) / 1e9)
                         torch.cuda.synchronize()
                         ok &= bool(torch.equal(out, blocks[:, :B])) and int(st.abs().sum()) == 0
+            if not DEC:
+                dr = {"-": [0.0]}
             er = [sorted(v)[len(v) // 2] for v in er.values()]
             dr = [sorted(v)[len(v) // 2] for v in dr.values()]
             print(f"{n:>2} {k:>2} {S:>6} {B:>8} {ps:>7} {(S + 1) // 2:>11} | " + " ".join(f"{x:6.0f}" for x in er) + " |              "
