@@ -376,10 +376,6 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
 // traffic for the 16k-byte stride of a 16-rows-per-lane form).  The
 // selection and W come from k_decode_prep (work: k slot numbers, then W
 // row-major).
-#ifndef WIDE_DEC_B96
-#define WIDE_DEC_B96 1
-#endif
-typedef u32 u32x3 __attribute__((ext_vector_type(3)));
 template <int K>
 __global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work, const int32_t *status,
                                                      u32 nslices, u32 slice_rows)
@@ -455,24 +451,11 @@ __global__ __launch_bounds__(256) void k_decode_wide(nkfs_geom g, const u8 *work
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
                     const u32 x = (p[q][c] >> (8 * rr)) & 0xFFu;
-                    const u8 *e = tbl + tdep + c * TB + x * 16;
-                    if constexpr (K <= 8 && WIDE_DEC_B96) {
-                        const uint2 t = *reinterpret_cast<const uint2 *>(e);
-                        row[rr][0] ^= t.x;
-                        row[rr][1] ^= t.y;
-                    } else if constexpr (K <= 12 && WIDE_DEC_B96) {
-                        // 12 output bytes: ds_read_b96, three banks per lane instead of four
-                        const u32x3 t = *reinterpret_cast<const u32x3 *>(e);
-                        row[rr][0] ^= t.x;
-                        row[rr][1] ^= t.y;
-                        row[rr][2] ^= t.z;
-                    } else {
-                        const uint4 t = *reinterpret_cast<const uint4 *>(e);
-                        row[rr][0] ^= t.x;
-                        row[rr][1] ^= t.y;
-                        row[rr][2] ^= t.z;
-                        row[rr][3] ^= t.w;
-                    }
+                    const uint4 t = *reinterpret_cast<const uint4 *>(tbl + tdep + c * TB + x * 16);
+                    row[rr][0] ^= t.x;
+                    row[rr][1] ^= t.y;
+                    row[rr][2] ^= t.z;
+                    row[rr][3] ^= t.w;
                 }
             }
             // rows rw + 256q + 4l .. +3 = run bytes [4K l, 4K l + 4K)

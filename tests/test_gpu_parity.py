@@ -713,8 +713,10 @@ def test_ragged_host_pipeline(L, O, n, k, chunk):
 def test_ragged_kernels_match(L, O, n, k, gap, order):
     """A ragged n <= 8 batch (sizes on either side of 64 KiB parts, 1 MiB,
     4 KiB, 1 byte, odd sizes) gives the same parts and digests from the walk
-    encoder (the ragged default: one wave per stripe), the fused kernel and
-    the warp-specialised kernel, launched largest-first or in batch order
+    encoder (the ragged default: one wave per stripe), the fused kernel, the
+    warp-specialised kernel (one or two hash waves) and the ragged split
+    across the two (part-size windows at 64 KiB, 13,108 B = C5's 64 KiB
+    stripes, 1 B = every stripe on ws), launched largest-first or in batch order
     (struct nkfs_tune size_order), aligned or not; digests of a sample
     against the oracle (crt/nk8.c:344-444, crt/xxhash.c:358-496)."""
     from nkfs_amd import batch
@@ -725,8 +727,12 @@ def test_ragged_kernels_match(L, O, n, k, gap, order):
         hb[boff[s_]: boff[s_] + Bs] = synth.stripe_bytes(1300 + s_, int(Bs))
     rid = synth.batch_ids(len(sizes), n, first=1300)
     outs = []
-    for kern, hw in (("walk", 1), ("fused", 1), ("ws", 1), ("ws", 2)):
-        with _tuned(enc_kernel=_enc(kern), size_order=order, enc_ws_hash_waves=hw):
+    # ("walk", hw, split): the ragged split -- stripes whose parts reach
+    # `split` bytes on the warp-specialised kernel, the rest on the walk
+    # encoder, two launches over complementary part-size windows
+    for kern, hw, split in (("walk", 1, 0), ("fused", 1, 0), ("ws", 1, 0), ("ws", 2, 0), ("walk", 1, 65536),
+                            ("walk", 2, 65536), ("walk", 2, 13108), ("walk", 1, 1)):
+        with _tuned(enc_kernel=_enc(kern), size_order=order, enc_ws_hash_waves=hw, enc_ragged_split=split):
             parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
             dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
             batch.encode_ragged(dev(hb), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(rid), parts, dev(poff),
