@@ -39,6 +39,30 @@ __host__ __device__ inline uint64_t xxh_round(uint64_t acc, uint64_t w)
     return rotl64_31(acc + w * XP2) * XP1;
 }
 
+// N rounds over w[0..N) of which the first `valid` count (valid <= 0: none).
+// Whole chunks -- every chunk but a message's last -- take the plain chain;
+// only a partial chunk pays a compare and two selects per round.
+// NKFS_XXH_SELECT=1 forces the select form everywhere (A/B builds).
+#ifndef NKFS_XXH_SELECT
+#define NKFS_XXH_SELECT 0
+#endif
+template <int N>
+__device__ inline uint64_t xxh_rounds(uint64_t acc, const uint64_t (&w)[N], int valid)
+{
+    if (!NKFS_XXH_SELECT && valid >= N) {
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+            acc = xxh_round(acc, w[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            const uint64_t nx = xxh_round(acc, w[r]);
+            acc = r < valid ? nx : acc;
+        }
+    }
+    return acc;
+}
+
 // Initial value of accumulator a (0..3) for a seed (xxhash.c:566-577).
 __host__ __device__ inline uint64_t xxh_acc_init(int a, uint64_t seed)
 {

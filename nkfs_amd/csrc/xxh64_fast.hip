@@ -264,11 +264,7 @@ __global__ __launch_bounds__(64) void k_xxh64_fast(Src src, u64 seed, u64 *out, 
         if (Src::kPaged)
             bases(b, c + 4);
         const u64 first = u64(c) * (CH / 32);
-#pragma unroll
-        for (int r = 0; r < CH / 32; ++r) {
-            const u64 nxt = xxh_round(acc, hw[r]);
-            acc = first + r < nst ? nxt : acc;
-        }
+        acc = xxh_rounds<CH / 32>(acc, hw, first >= nst ? 0 : int(min(nst - first, u64(CH / 32))));
     };
     for (u32 c = 0; c < wchunks; c += 2) {
         step(d0, b0, c);
@@ -379,11 +375,7 @@ __global__ __launch_bounds__(64) void k_xxh64_ring(Src src, u64 seed, u64 *out, 
         for (int r = 0; r < CH / 32; ++r)
             hw[r] = *reinterpret_cast<const u64 *>(slot + hoff[r]);
         const u64 first = u64(c) * (CH / 32);
-#pragma unroll
-        for (int r = 0; r < CH / 32; ++r) {
-            const u64 nxt = xxh_round(acc, hw[r]);
-            acc = first + r < nst ? nxt : acc;
-        }
+        acc = xxh_rounds<CH / 32>(acc, hw, first >= nst ? 0 : int(min(nst - first, u64(CH / 32))));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
 

@@ -86,6 +86,10 @@ def main():
                     res.setdefault(vi, {"ok": None})
                 res[vi].setdefault("e", []).append(enc_b / te / 1e9)
                 res[vi].setdefault("d", []).append(dec_b / td / 1e9)
+        if os.environ.get("AB_BOX"):  # this box's own stream for the encode's read:write mix (bench.box_stream)
+            from bench import box_stream
+            bx = box_stream(blocks, parts, B, n * ps, torch.cuda.current_stream())
+            print(f"{name} box stream {bx}", flush=True)
         for vi, v in enumerate(variants):
             e, d = sorted(res[vi]["e"]), sorted(res[vi]["d"])
             print(f"{name} {str(v):60s} enc {e[len(e)//2]:7.0f} ({e[0]:.0f}-{e[-1]:.0f})  "
