@@ -182,7 +182,10 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
 // one workgroup, and the parts are never read back (the two-pass form
 // re-read them: W1 PMC traffic 1.57x).  The group workgroups of a stripe
 // sit on one XCD (b mod 8) and share its block's lines in L2.
-template <int K, int NE>
+// PF: chunks of block loads in flight per encoder lane (1: the next chunk's
+// loads issue after this chunk's lookups; 2: two register sets rotate, so
+// a chunk's loads have two chunk periods to arrive).
+template <int K, int NE, int PF>
 __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g, const u8 *ids, u64 *digests,
                                                                   u32 ngroups)
 {
@@ -214,29 +217,31 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
         const u32 rbase = u32(wave) * 256u + 4u * u32(lane);  // this lane's first row in every chunk
         const bool aligned =
             ((reinterpret_cast<uintptr_t>(v.blk) | reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 15) == 0;
-        u32 d[K];  // 4 rows x K bytes
-        auto load_task = [&](u32 r0) {
+        u32 d[PF][K];  // 4 rows x K bytes per register set
+        auto load_task = [&](u32 (&x)[K], u32 r0) {
             const u64 off = u64(r0) * K;
             if (aligned && off + 4 * K <= v.B) {
                 const u32 *src = reinterpret_cast<const u32 *>(v.blk + off);
 #pragma unroll
                 for (int q = 0; q < K; ++q)
-                    d[q] = src[q];
+                    x[q] = src[q];
             } else {
 #pragma unroll
                 for (int q = 0; q < K; ++q) {
-                    u32 x = 0;
+                    u32 y = 0;
                     for (int e = 0; e < 4; ++e) {
                         const u64 p = off + 4 * q + e;
                         if (p < v.B)
-                            x |= u32(v.blk[p]) << (8 * e);
+                            y |= u32(v.blk[p]) << (8 * e);
                     }
-                    d[q] = x;
+                    x[q] = y;
                 }
             }
         };
-        if (rbase < v.ps)
-            load_task(rbase);  // first chunk requested before the table build
+#pragma unroll
+        for (int p = 0; p < PF; ++p)  // first chunks requested before the table build
+            if (rbase + u32(p) * CR < v.ps)
+                load_task(d[p], rbase + u32(p) * CR);
         // tables T_m, m = 1..K-1, of the group's parts, split over the
         // encoder waves (coefficient 0 past n: nothing is stored for those)
         u32 idw[4] = {0, 0, 0, 0};
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
         }
         __syncthreads();
 
-        for (u32 c = 0; c < nch; ++c) {
+        auto chunk = [&](u32 (&d)[K], u32 c) {
             const u32 r0 = c * CR + rbase;
             if (r0 < v.ps) {
                 // rows r0..r0+3: the m = 0 term is the byte itself (x^0 = 1)
@@ -283,8 +288,8 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
                     rows[rr][3] = e.w;
                     asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
                 }
-                if (r0 + CR < v.ps)
-                    load_task(r0 + CR);  // next chunk's rows in flight under this chunk's stores
+                if (r0 + PF * CR < v.ps)
+                    load_task(d, r0 + PF * CR);  // chunk c + PF's rows in flight under what follows
                 // 4 rows x 16 parts -> 16 parts x 4 rows (one dword each)
                 u32 out[16];
 #pragma unroll
@@ -308,6 +313,12 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
             }
             __syncthreads();  // chunk c is in the exchange
             __syncthreads();  // the hash wave has copied it
+        };
+        for (u32 c = 0; c < nch; c += PF) {
+            chunk(d[0], c);
+            if constexpr (PF == 2)
+                if (c + 1 < nch)
+                    chunk(d[PF - 1], c + 1);
         }
         return;
     }
@@ -573,11 +584,17 @@ extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint6
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
     const dim3 gd = dim3(u32(grid));
+    // chunks of loads in flight per encoder lane: struct nkfs_tune.enc_ws_prefetch
+    const int pf = nkfs_tune_now().enc_ws_prefetch;
     switch (k) {
 #define NKFS_K(KK, NE)                                                                                    \
     case KK:                                                                                              \
-        hipLaunchKernelGGL((k_encode_wide_ws<KK, NE>), gd, dim3(64 * (NE + 1)), 0, st, *g, ids, digests,  \
-                           u32(ngroups));                                                                 \
+        if (pf >= 2)                                                                                      \
+            hipLaunchKernelGGL((k_encode_wide_ws<KK, NE, 2>), gd, dim3(64 * (NE + 1)), 0, st, *g, ids, digests, \
+                               u32(ngroups));                                                             \
+        else                                                                                              \
+            hipLaunchKernelGGL((k_encode_wide_ws<KK, NE, 1>), gd, dim3(64 * (NE + 1)), 0, st, *g, ids, digests, \
+                               u32(ngroups));                                                             \
         break;
         // three encoder waves + the hash wave = 256 threads: a 320-thread
         // workgroup (four encoder waves) stayed alone on its CU (SQ: ~5

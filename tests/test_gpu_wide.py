@@ -76,6 +76,8 @@ def test_wide_encode_matches(L, O, n, k, B, S):
         p2, _ = batch.encode(blocks, B, n, k, ids, digests=False)
     with _tuned(enc_kernel=_enc("wide_ws")):  # XXH64 fused (hash wave)
         p4, d4 = batch.encode(blocks, B, n, k, ids)
+    with _tuned(enc_kernel=_enc("wide_ws"), enc_ws_prefetch=2):  # two chunks of loads in flight
+        p5, d5 = batch.encode(blocks, B, n, k, ids)
     p3, d3 = batch.encode(blocks, B, n, k, ids)  # default dispatch
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
@@ -83,6 +85,7 @@ def test_wide_encode_matches(L, O, n, k, B, S):
     assert torch.equal(p0[:, :ps], p2[:, :ps])
     assert torch.equal(p0[:, :ps], p3[:, :ps]) and torch.equal(d0, d3)
     assert torch.equal(p0[:, :ps], p4[:, :ps]) and torch.equal(d0, d4)
+    assert torch.equal(p0[:, :ps], p5[:, :ps]) and torch.equal(d0, d5)
     got = [u64(x) for x in d1.cpu().tolist()]
     for s in sorted({0, S // 2, S - 1}):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
@@ -109,16 +112,17 @@ def test_wide_encode_ragged(L, O, n, k, gap):
         host[boff[s]: boff[s] + B] = synth.stripe_bytes(700 + s, int(B))
     ids_np = synth.batch_ids(len(sizes), n, first=700)
     outs = []
-    for kern in ("generic", "wide", "wide_ws"):
+    for kern, pf in (("generic", 1), ("wide", 1), ("wide_ws", 1), ("wide_ws", 2)):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-        with _tuned(enc_kernel=_enc(kern)):
+        with _tuned(enc_kernel=_enc(kern), enc_ws_prefetch=pf):
             batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts,
                                 dev(poff), dig, int(sizes.max()))
         torch.cuda.synchronize()
         outs.append((parts.cpu().numpy(), [u64(x) for x in dig.cpu().tolist()]))
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
     assert np.array_equal(outs[0][0], outs[2][0]) and outs[0][1] == outs[2][1]
+    assert np.array_equal(outs[0][0], outs[3][0]) and outs[0][1] == outs[3][1]
     pn, got = outs[1]
     for s in (0, 2, 3, 4, len(sizes) - 1):
         B = int(sizes[s])
