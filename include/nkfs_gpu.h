@@ -85,7 +85,8 @@ struct nkfs_tune {
 	int enc_fused_waves_per_cu; /* fused encoder: resident waves per CU cap (0 = none, 3..32) */
 	int dec_wave_waves_per_cu;  /* wave-per-stripe decoder: same cap */
 	int dec_run_units;    /* run decoder: 1,024-row units per chunk (1, 2, 4, 8, 16) */
-	int enc_ws_prefetch;  /* warp-specialised encoder, n > 4: chunks of loads in flight per encoder wave (1, 2) */
+	int enc_ws_prefetch;  /* warp-specialised encoders (n > 4, and the n > 8 fused part-group encoder): chunks of
+	                         loads in flight per encoder wave (1, 2; default 2) */
 	int enc_big_fused;    /* k > 16 encoder: 1 = XXH64 fused (traffic 1.0x, ~6 % slower on W2), 0 = second pass (default) */
 	int dec_pair_stage;   /* k = 2 decoder: 1 = output through an LDS stage (1 KiB runs per store), 0 = direct */
 	int host_depth;       /* host-memory entry points: sub-batches in flight per lane (2..8) */
