@@ -365,7 +365,10 @@ extern "C" int nkfs_fast_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // KiB and up, or at most 1,024 stripes: N4K2 65,536 x 16 KiB ws 5,816 /
     // fused 4,960, 1,024 x 64 KiB 4,206 / 1,616, 1,024 x 4 KiB 1,336 / 911;
     // C2 (65,536 x 4 KiB) stays fused 5,237 / ws 4,332 (seam_sweep_box2.txt).
-    if (rules && digests && (ps >= 8192 || (E == 4 && !g->block_sizes && g->nstripes <= 1024)))
+    // Round 4: n > 4 from 4 KiB parts on <= 1,024 stripes as well (walk_by_rule).
+    if (rules && digests &&
+        (ps >= 8192 || (E == 4 && !g->block_sizes && g->nstripes <= 1024) ||
+         (E == 8 && ps >= 4096 && g->nstripes <= 1024)))
         return nkfs_ws_encode(g, ids, digests, 4, false, st);
     // Nibble tables free LDS (N8K5: 25 -> 11 KB per wave, the occupancy
     // limit) at twice the lookups: a win where the grid offers more waves

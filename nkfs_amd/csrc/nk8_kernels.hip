@@ -682,12 +682,17 @@ static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
     // ws2 4,960 / walk 4,901, 2,048 x 256 KiB 4,650 / 4,549; 131,072-byte
     // blocks (26 KiB parts) stay on the walk encoder, 4,764 / 4,875
     // (profiles/r04/seam_ws2.txt).
+    // Round 4 (seam_mid.txt, seam_sweep_r04_boxA.txt): up to 1,024 stripes
+    // the warp-specialised grid fits one round of workgroups and wins from
+    // 4 KiB parts (N8K5 512 x 128 KiB 3,713 / walk 2,388, 1,024 x 64 KiB
+    // 4,329 / 3,781, 256 x 20 KiB 1,028 / 763; 1 KiB parts stay on the walk,
+    // 767 / 921).
     if (g->block_sizes || !digests || g->n <= 4)
         return 0;
     const u32 ps = (g->block_size + u32(g->k) - 1) / u32(g->k);
-    const bool ws2 = g->nstripes >= 1024 && nkfs_tune_now().enc_ws_hash_waves != 1;
-    const bool ws = ps >= 65536 || (ps >= 32768 && g->nstripes <= 1024) || (ps >= 8192 && g->nstripes <= 256) ||
-                    (ws2 && ps >= 49152);
+    const int hwt = nkfs_tune_now().enc_ws_hash_waves;
+    const bool ws2 = hwt == 2 || (!hwt && nkfs_ws_auto_hash_waves(g->nstripes) == 2);
+    const bool ws = ps >= 65536 || (ps >= 4096 && g->nstripes <= 1024) || (ws2 && ps >= 49152);
     return !ws;
 }
 

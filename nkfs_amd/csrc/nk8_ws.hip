@@ -336,9 +336,9 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
     int rc;
     // chunks of loads in flight per encoder wave (struct nkfs_tune.enc_ws_prefetch)
     // n > 4: struct nkfs_tune.enc_ws_hash_waves picks one or two hash waves
-    // per workgroup (0: two from 1,024 stripes on, where the grid of four-
-    // stripe workgroups still fills the chip: N8K5 1,024-16,384 x 512 KiB
-    // +1-4 %, 16,384 x 256 KiB +1-6 %, 256 stripes -30 %; seam_ws2.txt);
+    // per workgroup (0: nkfs_ws_auto_hash_waves -- two where the grid of
+    // four-stripe workgroups ends no later: N8K5 768 x 64 KiB 3,445 / 2,474,
+    // 8,192 x 512 KiB +1-4 %, 512 x 128 KiB 2,958 / 3,713; seam_mid.txt);
     // n > 4: struct nkfs_tune.enc_ws_waves overrides the caller's 4 encoder
     // waves with 6 (three per stripe, 3,072-row chunks: the exchange then
     // holds 99 KiB and the workgroup 7 waves, one per CU as before, with half
@@ -350,7 +350,7 @@ extern "C" int nkfs_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *
     if (g->n <= 4)
         rc = ne == 8 ? launch_ws<4, 8, false, 1>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<4, 4, false, 1>(g->k, st, *g, ids, digests, nt);
-    else if (ne == 4 && (t.enc_ws_hash_waves == 2 || (!t.enc_ws_hash_waves && g->nstripes >= 1024)))
+    else if (ne == 4 && (t.enc_ws_hash_waves == 2 || (!t.enc_ws_hash_waves && nkfs_ws_auto_hash_waves(g->nstripes) == 2)))
         rc = pf >= 2 ? launch_ws<8, 4, false, 2, 2>(g->k, st, *g, ids, digests, nt)
                      : launch_ws<8, 4, false, 1, 2>(g->k, st, *g, ids, digests, nt);
     else if (ne == 6)

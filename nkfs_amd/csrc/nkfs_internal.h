@@ -54,6 +54,17 @@ struct nkfs_geom {
  * in all (sum over stripes of ceil(part_size / 1024)). */
 uint64_t nkfs_ragged_scratch_bytes(uint32_t nstripes, uint64_t sum_units);
 
+/* Hash waves per warp-specialised workgroup (n > 4) for a batch of s
+ * stripes: one CU holds one workgroup, so a grid that ends in a partial
+ * round of workgroups wastes CUs.  Two hash waves (four stripes per
+ * workgroup) whenever their rounds, at twice the work each, take no longer
+ * than one hash wave's: 768 / 1,024 / 8,192 stripes -> 2; 384 / 512 /
+ * 1,536 -> 1 (profiles/r04/seam_mid.txt, seam_sweep_r04_boxA.txt). */
+static inline int nkfs_ws_auto_hash_waves(uint32_t s)
+{
+	return 2u * ((s + 1023u) / 1024u) <= (s + 511u) / 512u ? 2 : 1;
+}
+
 /* Kernel choice and launch shape (struct nkfs_tune, include/nkfs_gpu.h):
  * one process-wide copy, set at init, read by the launchers. */
 struct nkfs_tune;

@@ -37,7 +37,9 @@ def main():
     _lib.check(L.nkfs_gpu_init(0))
     shapes = [(8, 5, B, S) for B in (65536, 131072, 262144, 524288, 1048576)
               for S in ((256, 1024, 2048, 4096, 8192, 16384) if not quick else (1024, 4096))]
-    if os.environ.get("SWEEP_SHAPES") != "n8":
+    if os.environ.get("SWEEP_SHAPES") == "mid":  # the warp-specialised / walk seam below 2,048 stripes
+        shapes = [(8, 5, B, S) for B in (20480, 65536, 131072, 262144) for S in (256, 384, 512, 768, 1024, 1536)]
+    elif os.environ.get("SWEEP_SHAPES") != "n8":
         shapes += [(4, 2, B, S) for B in (4096, 16384, 65536, 262144) for S in (1024, 8192, 65536)]
         shapes += [(8, 5, B, S) for B in (4096, 20480) for S in (1024, 8192, 65536)]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "3"))
