@@ -528,13 +528,16 @@ def test_warp_specialised_encode_matches(L, n, k, B, hw):
         assert torch.equal(d0, d1), S
 
 
-@pytest.mark.parametrize("S,B", [(2200, 163840), (3500, 131072), (1700, 1048576)])
+@pytest.mark.parametrize("S,B", [(2200, 163840), (3500, 131072), (1700, 1048576), (768, 65536), (513, 20480),
+                                 (300, 20480), (1536, 262144), (1025, 262144)])
 def test_encode_dispatch_shapes_agree(L, O, S, B):
     """Grids the default dispatch sends to different kernels (N8K5: 1,100
     fused waves of 32 KiB parts -> warp-specialised; 1,750 waves of 26 KB
-    parts -> nibble tables; 850 waves of 1 MiB stripes -> warp-specialised),
-    and the walk encoder, give the same parts and digests as the fused
-    256-entry-table kernel, and the oracle's on the first and last stripe."""
+    parts -> nibble tables; 850 waves of 1 MiB stripes -> warp-specialised;
+    round 4: 768 / 513 stripes -> two hash waves, 300 -> one, 1,536 x 256
+    KiB -> walk, partial last workgroups), and the walk encoder, give the
+    same parts and digests as the fused 256-entry-table kernel, and the
+    oracle's on the first and last stripe."""
     from nkfs_amd import batch
     n, k = 8, 5
     blocks = batch.synth(S, B, first=5)
