@@ -62,7 +62,7 @@ uint64_t nkfs_ragged_scratch_bytes(uint32_t nstripes, uint64_t sum_units);
  * 1,536 -> 1 (profiles/r04/seam_mid.txt, seam_sweep_r04_boxA.txt). */
 static inline int nkfs_ws_auto_hash_waves(uint32_t s)
 {
-	return 2u * ((s + 1023u) / 1024u) <= (s + 511u) / 512u ? 2 : 1;
+	return 2ull * (((uint64_t)s + 1023u) / 1024u) <= ((uint64_t)s + 511u) / 512u ? 2 : 1;
 }
 
 /* Kernel choice and launch shape (struct nkfs_tune, include/nkfs_gpu.h):
