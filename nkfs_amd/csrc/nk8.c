@@ -120,9 +120,8 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 		memcpy(h, block, B);
 		memcpy(h + off_ids, ids, (size_t)n);
 		struct nkfs_geom zg = { h, round16(B), B, NULL, NULL, h + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
-		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)))
+		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)) || (err = nkfs_ctx_wait(c)))
 			goto out;
-		HIPGO(hipStreamSynchronize(c->stream));
 		for (int i = 0; i < n; i++)
 			memcpy(parts[i], h + off_parts + pitch * (uint64_t)i, ps);
 		err = 0;
@@ -230,9 +229,9 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 		struct nkfs_geom zg = { h + off_block, round16(block_size), block_size, NULL, NULL, h + off_parts, pitch,
 					NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0 };
 		if ((err = nkfs_launch_decode(&zg, k, h + off_ids, h + off_avail, k, h + off_work,
-					      (int32_t *)(h + off_status), nkfs_gf(), c->stream, NULL, NULL)))
+					      (int32_t *)(h + off_status), nkfs_gf(), c->stream, NULL, NULL)) ||
+		    (err = nkfs_ctx_wait(c)))
 			goto out;
-		HIPGO(hipStreamSynchronize(c->stream));
 		int32_t zst;
 		memcpy(&zst, h + off_status, sizeof(zst));
 		if (!zst)

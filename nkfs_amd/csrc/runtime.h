@@ -19,6 +19,8 @@ struct nkfs_ctx {
 	hipEvent_t ev[2]; /* created on first use (nkfs_ctx_events) */
 	int nev;
 	uint64_t seq;     /* completion words handed out on this context */
+	volatile uint64_t *done; /* pinned completion word (nkfs_ctx_wait; first use) */
+	void *ddone;      /* its device-visible address */
 	struct nkfs_ctx *next;
 };
 
@@ -28,6 +30,7 @@ void nkfs_ctx_put(struct nkfs_ctx *c);
 int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_events(struct nkfs_ctx *c); /* c->ev[0..1] exist afterwards */
+int nkfs_ctx_wait(struct nkfs_ctx *c);   /* everything enqueued on c->stream is done (spin, see runtime.c) */
 const void *nkfs_gf(void);                   /* tables on the library's device */
 const void *nkfs_gf_on(int dev);
 const void *nkfs_gf_for(void *stream);       /* tables on the device of `stream` */
