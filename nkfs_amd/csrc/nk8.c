@@ -101,6 +101,8 @@ static uint64_t round16(uint64_t v) { return (v + 15) & ~(uint64_t)15; }
 #ifndef NKFS_ZC_MAX
 #define NKFS_ZC_MAX 1048576
 #endif
+/* blocks from this size wait by spinning on a completion word (nkfs_ctx_wait) */
+#define NKFS_SPIN_MIN 32768
 
 static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8_t *ids, uint8_t **parts)
 {
@@ -120,7 +122,8 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 		memcpy(h, block, B);
 		memcpy(h + off_ids, ids, (size_t)n);
 		struct nkfs_geom zg = { h, round16(B), B, NULL, NULL, h + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
-		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)) || (err = nkfs_ctx_wait(c)))
+		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)) ||
+		    (err = nkfs_ctx_wait(c, B >= NKFS_SPIN_MIN)))
 			goto out;
 		for (int i = 0; i < n; i++)
 			memcpy(parts[i], h + off_parts + pitch * (uint64_t)i, ps);
@@ -138,7 +141,8 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 	if ((err = nkfs_launch_encode(&g, d + off_ids, NULL, nkfs_gf(), c->stream)))
 		goto out;
 	HIPGO(hipMemcpyAsync(h, d + off_parts, parts_bytes, hipMemcpyDeviceToHost, c->stream));
-	HIPGO(hipStreamSynchronize(c->stream));
+	if ((err = nkfs_ctx_wait(c, 1)))
+		goto out;
 	for (int i = 0; i < n; i++)
 		memcpy(parts[i], h + pitch * (uint64_t)i, ps);
 	err = 0;
@@ -230,7 +234,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 					NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0 };
 		if ((err = nkfs_launch_decode(&zg, k, h + off_ids, h + off_avail, k, h + off_work,
 					      (int32_t *)(h + off_status), nkfs_gf(), c->stream, NULL, NULL)) ||
-		    (err = nkfs_ctx_wait(c)))
+		    (err = nkfs_ctx_wait(c, block_size >= NKFS_SPIN_MIN)))
 			goto out;
 		int32_t zst;
 		memcpy(&zst, h + off_status, sizeof(zst));
@@ -255,7 +259,8 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 				      (int32_t *)(d + off_status), nkfs_gf(), c->stream, NULL, NULL)))
 		goto out;
 	HIPGO(hipMemcpyAsync(h, d + off_status, 16 + block_size, hipMemcpyDeviceToHost, c->stream));
-	HIPGO(hipStreamSynchronize(c->stream));
+	if ((err = nkfs_ctx_wait(c, 1)))
+		goto out;
 	int32_t st;
 	memcpy(&st, h, sizeof(st));
 	if (!st)

@@ -447,14 +447,19 @@ int nkfs_ctx_events(struct nkfs_ctx *c)
  * work is done (hipStreamWriteValue64 orders after it, the kernels' host
  * writes released at system scope), and the host spins on that word.  The
  * stream's status is polled now and then, so a failed launch cannot spin
- * forever.  A one-block drop-in call waits here; the
- * stream sync's wake-up costs several microseconds of a ~15 us call. */
-int nkfs_ctx_wait(struct nkfs_ctx *c)
+ * forever.  The one-block drop-in calls wait here: the extra stream packet
+ * costs ~4 us on a 4 KiB call, where the stream sync still spins, but the
+ * sync's later wake-up costs 2-28 us from 64 KiB blocks on
+ * (profiles/r04/percall_spin_vs_sync.txt), so callers spin from 32 KiB. */
+int nkfs_ctx_wait(struct nkfs_ctx *c, int spin)
 {
 #ifdef NKFS_WAIT_SYNC /* A/B builds: the plain stream sync */
-	HIPCHK(hipStreamSynchronize(c->stream));
-	return 0;
+	spin = 0;
 #endif
+	if (!spin) {
+		HIPCHK(hipStreamSynchronize(c->stream));
+		return 0;
+	}
 	if (!c->done) {
 		void *h = NULL, *d = NULL;
 		HIPCHK(hipHostMalloc(&h, 64, hipHostMallocDefault));

@@ -30,7 +30,9 @@ void nkfs_ctx_put(struct nkfs_ctx *c);
 int nkfs_ctx_dev(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_host(struct nkfs_ctx *c, size_t bytes, void **out);
 int nkfs_ctx_events(struct nkfs_ctx *c); /* c->ev[0..1] exist afterwards */
-int nkfs_ctx_wait(struct nkfs_ctx *c);   /* everything enqueued on c->stream is done (spin, see runtime.c) */
+/* everything enqueued on c->stream is done: a spin on a stream-written word
+ * when `spin`, else the stream sync (runtime.c) */
+int nkfs_ctx_wait(struct nkfs_ctx *c, int spin);
 const void *nkfs_gf(void);                   /* tables on the library's device */
 const void *nkfs_gf_on(int dev);
 const void *nkfs_gf_for(void *stream);       /* tables on the device of `stream` */
