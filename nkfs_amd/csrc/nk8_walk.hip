@@ -537,17 +537,23 @@ __global__ __launch_bounds__(64, 2) void k_encode_walk(nkfs_geom g, const u8 *id
 
 // ------------------------------------------------------------------ decode
 //
-// k_decode_plan: lane per stripe.  First K offered slots with distinct ids
-// (crt/nk8.c:512-537) and W = V^-1 for V[m][c] = x_c^m in closed form
-// (Lagrange basis: W[c][m] = [t^m] M(t)/(t + x_c) / M'(x_c) with
-// M(t) = prod_c (t + x_c)): the unique inverse, so identical to the
-// reference's Gauss-Jordan (crt/nk8.c:199-266).  plan[s] = K slots then W
-// row-major; slot byte 0xFF marks a stripe with fewer than K distinct ids.
+// k_decode_plan: K lanes per stripe, lane c of a stripe computes row c of
+// W.  First K offered slots with distinct ids (crt/nk8.c:512-537) and
+// W = V^-1 for V[m][c] = x_c^m in closed form (Lagrange basis: W[c][m] =
+// [t^m] M(t)/(t + x_c) / M'(x_c) with M(t) = prod_c (t + x_c)): the unique
+// inverse, so identical to the reference's Gauss-Jordan
+// (crt/nk8.c:199-266).  plan[s] = K slots then W row-major; slot byte 0xFF
+// marks a stripe with fewer than K distinct ids.  The plan is a serial chain
+// of bit-serial GF products on one lane, so spreading the K rows over K
+// lanes (and loading the first 16 offers before walking them) cuts the
+// kernel -- a fixed cost of every uniform k >= 3 decode -- from ~9 us.
 template <int K>
 __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *avail, int n_slots, int navail,
                                                      u32 nstripes, u8 *plan, int32_t *status, const GfTables *gft)
 {
-    const u32 s = blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 t = u64(blockIdx.x) * blockDim.x + threadIdx.x;
+    const u32 s = u32(t / K);
+    const int col = int(t % K);
     if (s >= nstripes)
         return;
     const u8 *sid = ids + u64(s) * n_slots;
@@ -555,15 +561,13 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
     u8 *pl = plan + u64(s) * (K + K * K);
     u32 x[K], sl[K];
     int h = 0;
-    for (int c = 0; c < navail && h < K; ++c) {
-        const u32 slot = sav[c];
-        const u32 id = sid[slot];
+    auto offer = [&](u32 slot, u32 id) {
         bool dup = false;
 #pragma unroll
         for (int j = 0; j < K; ++j)
             dup |= j < h && x[j] == id;
-        if (dup)
-            continue;
+        if (dup || h >= K)
+            return;
 #pragma unroll
         for (int j = 0; j < K; ++j)
             if (j == h) {
@@ -571,11 +575,29 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
                 sl[j] = slot;
             }
         ++h;
+    };
+    // the first 16 offers: all loads issued before any is used
+    constexpr int PRE = 16;
+    u32 pslot[PRE], pid[PRE];
+#pragma unroll
+    for (int c = 0; c < PRE; ++c)
+        pslot[c] = c < navail ? sav[c] : 0u;
+#pragma unroll
+    for (int c = 0; c < PRE; ++c)
+        pid[c] = c < navail ? sid[pslot[c]] : 0u;
+#pragma unroll
+    for (int c = 0; c < PRE; ++c)
+        if (c < navail)
+            offer(pslot[c], pid[c]);
+    for (int c = PRE; c < navail && h < K; ++c) {
+        const u32 slot = sav[c];
+        offer(slot, sid[slot]);
     }
-    if (status)
+    if (col == 0 && status)
         status[s] = h < K ? -EINVAL : 0;
     if (h < K) {
-        pl[0] = 0xFF;
+        if (col == 0)
+            pl[0] = 0xFF;
         return;
     }
     u32 M[K + 1];
@@ -588,26 +610,31 @@ __global__ __launch_bounds__(256) void k_decode_plan(const u8 *ids, const u8 *av
             M[i] = M[i - 1] ^ gfm_bits(x[c], M[i]);
         M[0] = gfm_bits(x[c], M[0]);
     }
+    // this lane's row: x_c, slot of column col
+    u32 xc = 0, sc = 0;
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-        pl[c] = u8(sl[c]);
-        u32 q[K];
-        u32 a = M[K];
-        q[K - 1] = a;
-#pragma unroll
-        for (int i = K - 1; i >= 1; --i) {
-            a = M[i] ^ gfm_bits(x[c], a);
-            q[i - 1] = a;
+    for (int c = 0; c < K; ++c)
+        if (c == col) {
+            xc = x[c];
+            sc = sl[c];
         }
-        u32 dd = 0;
+    pl[col] = u8(sc);
+    u32 q[K];
+    u32 a = M[K];
+    q[K - 1] = a;
 #pragma unroll
-        for (int i = K - 1; i >= 0; --i)
-            dd = gfm_bits(dd, x[c]) ^ q[i];
-        const u32 dinv = gft->inv[dd];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            pl[K + c * K + i] = u8(gfm_bits(q[i], dinv));
+    for (int i = K - 1; i >= 1; --i) {
+        a = M[i] ^ gfm_bits(xc, a);
+        q[i - 1] = a;
     }
+    u32 dd = 0;
+#pragma unroll
+    for (int i = K - 1; i >= 0; --i)
+        dd = gfm_bits(dd, xc) ^ q[i];
+    const u32 dinv = gft->inv[dd];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        pl[K + col * K + i] = u8(gfm_bits(q[i], dinv));
 }
 
 // One-shot slice: rows [slice*R, slice*R + R) of one stripe, R = 1024*U.
@@ -1009,7 +1036,7 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         return 0;
     u8 *plan = static_cast<u8 *>(work);
     const GfTables *gft = static_cast<const GfTables *>(gf);
-    const dim3 pgrid((g->nstripes + 255) / 256);
+    const dim3 pgrid(u32((u64(g->nstripes) * u64(g->k) + 255) / 256));  // k_decode_plan: k lanes per stripe
     const u32 ps = part_size_of_host(g->block_size, g->k);  // ragged: the bound on block sizes
     units = units >= 4 ? 4 : units >= 2 ? 2 : 1;
     // a stripe that fits in fewer units takes one wave of just those
