@@ -98,9 +98,6 @@ struct nkfs_tune {
 	                         general kernels + a hash pass instead of one wave per stripe (0..63) */
 	int enc_ws_hash_waves; /* warp-specialised encoder, n > 4 with 4 encoder waves: hash waves per workgroup
 	                          (0 auto: 2 from 1,024 stripes on; 1; 2) */
-	int enc_big_overlap;   /* k > 16 unfused encode: stripe ranges whose XXH64 pass overlaps the next range's
-	                          encode on a side stream (0/1 = off, 2..16) */
-	int enc_big_hash_form; /* that pass: 0 by rule, 1 register form (fits beside the encoder), 2 ring form */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

@@ -743,71 +743,6 @@ static bool few_big_stripes(const nkfs_geom *g)
            g->nstripes <= u32(t.enc_few_max) && ps >= 1024;
 }
 
-extern "C" int nkfs_fast_xxh64_parts_form(const nkfs_geom *g, uint64_t *out, hipStream_t st, int form);
-
-// k > 16, uniform, second-pass XXH64: the batch in `chunks` consecutive
-// stripe ranges; range i's parts are hashed on a side stream while range
-// i + 1 is encoded.  The hash pass is latency-bound (one chain per lane,
-// 1,024 dependent rounds per 32 KiB part: few waves, most CUs idle) and the
-// column-chunked encoder is LDS-bound, so the two overlap.  Fork / join
-// through events, so the caller's stream orders everything (and a graph
-// capture sees the fork).  One side stream and event set per device,
-// enqueued under a lock.
-namespace {
-struct Side {
-    hipStream_t s = nullptr;
-    hipEvent_t ev[17] = {};
-};
-Side g_side[NKFS_MAX_DEVICES];
-std::mutex g_side_mu;
-}  // namespace
-
-static int big_encode_overlap(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
-                              hipStream_t st, int chunks, int form)
-{
-    int dev = 0;
-    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= NKFS_MAX_DEVICES)
-        return -ENOSYS;
-    std::lock_guard<std::mutex> lk(g_side_mu);
-    Side &sd = g_side[dev];
-    if (!sd.s) {
-        int cur = 0;
-        if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(dev) != hipSuccess)
-            return -ENOSYS;
-        bool ok = hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; ok && i < 17; ++i)
-            ok = hipEventCreateWithFlags(&sd.ev[i], hipEventDisableTiming) == hipSuccess;
-        (void)hipSetDevice(cur);
-        if (!ok)
-            return -EIO;
-    }
-    chunks = chunks > 16 ? 16 : chunks;
-    const u32 S = g->nstripes, per = (S + u32(chunks) - 1) / u32(chunks);
-    // the side stream starts after everything already on the caller's stream
-    if (hipEventRecord(sd.ev[16], st) != hipSuccess || hipStreamWaitEvent(sd.s, sd.ev[16], 0) != hipSuccess)
-        return -EIO;
-    int rc = 0, c = 0;
-    for (u32 a = 0; a < S && !rc; a += per, ++c) {
-        nkfs_geom gc = *g;
-        gc.nstripes = min(per, S - a);
-        gc.blocks = g->blocks + u64(a) * g->block_pitch;
-        gc.parts = g->parts + u64(a) * u64(g->n) * g->part_pitch;
-        gc.blocks_bytes = gc.parts_bytes = 0;
-        if ((rc = nkfs_big_encode(&gc, ids + u64(a) * u64(g->n), nullptr, gf, st)))
-            break;
-        if (hipEventRecord(sd.ev[c], st) != hipSuccess || hipStreamWaitEvent(sd.s, sd.ev[c], 0) != hipSuccess) {
-            rc = -EIO;
-            break;
-        }
-        rc = nkfs_fast_xxh64_parts_form(&gc, digests + u64(a) * u64(g->n), sd.s, form);
-    }
-    // join: the caller's stream waits for the last hash (also on failure, so
-    // nothing of this call is left running unordered)
-    if (hipEventRecord(sd.ev[16], sd.s) != hipSuccess || hipStreamWaitEvent(st, sd.ev[16], 0) != hipSuccess)
-        return -EIO;
-    return rc;
-}
-
 extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
                                   void *stream)
 {
@@ -846,15 +781,6 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         rc = digests && nkfs_tune_now().enc_big_fused ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
         if (rc != -ENOSYS)
             return rc;
-        // uniform batches with digests: hash range i while range i + 1 encodes
-        // (struct nkfs_tune.enc_big_overlap ranges; 0 = one range, then one pass)
-        const nkfs_tune t = nkfs_tune_now();
-        if (digests && !g->block_sizes && g->k > 16 && t.enc_big_overlap > 1 &&
-            g->nstripes >= u32(t.enc_big_overlap) && kern != NKFS_ENC_GENERIC) {
-            rc = big_encode_overlap(g, ids, digests, gf, st, t.enc_big_overlap, t.enc_big_hash_form);
-            if (rc != -ENOSYS)
-                return rc;
-        }
         rc = nkfs_big_encode(g, ids, nullptr, gf, st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);

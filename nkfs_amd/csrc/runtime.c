@@ -66,9 +66,7 @@ static struct nkfs_tune g_tune = {
 	.host_lanes = 2,  /* (profiles/r04/pcie.txt) */
 	.enc_ws_waves = 4,
 	.enc_few_max = 63,
-	.enc_ws_hash_waves = 0,
-	.enc_big_overlap = 0,
-	.enc_big_hash_form = 0, /* auto: 2 from 1,024 stripes (profiles/r04/seam_ws2.txt) */
+	.enc_ws_hash_waves = 0, /* auto: 2 from 1,024 stripes (profiles/r04/seam_ws2.txt) */
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
 
@@ -97,8 +95,7 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
 	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0 ||
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||
-	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2 ||
-	    t->enc_big_overlap < 0 || t->enc_big_overlap > 16 || t->enc_big_hash_form < 0 || t->enc_big_hash_form > 2)
+	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;

@@ -428,9 +428,7 @@ extern "C" int nkfs_fast_xxh64_list(const uint8_t *base, const uint64_t *off, co
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-// form: 0 by the waves-per-SIMD rule, 1 the register form (8.7 KB of LDS
-// per wave: fits beside other kernels' workgroups), 2 the ring form
-extern "C" int nkfs_fast_xxh64_parts_form(const nkfs_geom *g, uint64_t *out, hipStream_t st, int form)
+extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, uint64_t *out, hipStream_t st)
 {
     const u64 total = u64(g->nstripes) * u64(g->n);
     if (!total)
@@ -438,7 +436,7 @@ extern "C" int nkfs_fast_xxh64_parts_form(const nkfs_geom *g, uint64_t *out, hip
     PartsOf src{*g};
     // ragged part offsets are caller data: assume only 8-byte alignment there
     const bool a16 = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->parts) | g->part_pitch) & 15) == 0;
-    if (a16 && form != 1 && (form == 2 || use_ring(total))) {  // the DMA form needs 16-byte aligned pieces
+    if (a16 && use_ring(total)) {  // the DMA form needs 16-byte aligned pieces
         hipLaunchKernelGGL((k_xxh64_ring<PartsOf, 4>), dim3(u32((total + MSGS - 1) / MSGS)), dim3(64), 0, st, src,
                            u64(0), out, (const u64 *)nullptr, (int32_t *)nullptr);
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -446,11 +444,6 @@ extern "C" int nkfs_fast_xxh64_parts_form(const nkfs_geom *g, uint64_t *out, hip
     NKFS_XXH_LAUNCH(PartsOf, a16, dim3(u32((total + MSGS - 1) / MSGS)), st, src, u64(0), out, (const u64 *)nullptr,
                     (int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
-}
-
-extern "C" int nkfs_fast_xxh64_parts(const nkfs_geom *g, uint64_t *out, hipStream_t st)
-{
-    return nkfs_fast_xxh64_parts_form(g, out, st, 0);
 }
 
 extern "C" int nkfs_fast_xxh64_strided(const uint8_t *base, uint64_t pitch, uint64_t len, uint32_t count,
