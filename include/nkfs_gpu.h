@@ -142,7 +142,8 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
  * output (n_slots per stripe, pitch part_pitch); d_ids[s*n_slots + j] is the
  * id of slot j.  d_avail[s*navail + c] lists the slots offered for stripe s
  * in caller order; like nk8_assemble_block the first k with distinct ids
- * are used.  d_work: nkfs_decode_workspace(nstripes, k) bytes of device
+ * are used.  Every d_avail entry must be below n_slots (the host-memory
+ * forms check h_avail and return -EINVAL).  d_work: nkfs_decode_workspace(nstripes, k) bytes of device
  * scratch.  d_status[s] (may be NULL) receives 0 or -EINVAL (fewer than k
  * distinct ids) per stripe; such stripes are left unwritten. */
 uint64_t nkfs_decode_workspace(uint32_t nstripes, int k);

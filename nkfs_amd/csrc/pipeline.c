@@ -1178,9 +1178,22 @@ int nkfs_nk8_encode_pages(const uint8_t *const *h_pages, uint32_t page_size, con
 	return hp_run(&h);
 }
 
-static int dec_args_ok(int n_slots, int navail, int k, uint32_t block_size, const uint8_t *ids, const uint8_t *avail)
+/* every offered slot must exist: the kernels index the stripe's id row
+ * with it (a device-resident caller owns this precondition, nkfs_gpu.h) */
+static int avail_ok(const uint8_t *avail, uint32_t nstripes, int navail, int n_slots)
 {
-	return !nkfs_bad_params(block_size, navail, k) && n_slots >= 1 && n_slots <= 255 && ids && avail;
+	const uint64_t cnt = (uint64_t)nstripes * (uint64_t)navail;
+	for (uint64_t i = 0; i < cnt; i++)
+		if (avail[i] >= n_slots)
+			return 0;
+	return 1;
+}
+
+static int dec_args_ok(int n_slots, int navail, int k, uint32_t block_size, const uint8_t *ids, const uint8_t *avail,
+		       uint32_t nstripes)
+{
+	return !nkfs_bad_params(block_size, navail, k) && n_slots >= 1 && n_slots <= 255 && ids && avail &&
+	       avail_ok(avail, nstripes, navail, n_slots);
 }
 
 int nkfs_nk8_decode_host(const uint8_t *h_parts, uint64_t part_pitch, int n_slots, const uint8_t *h_ids,
@@ -1188,7 +1201,7 @@ int nkfs_nk8_decode_host(const uint8_t *h_parts, uint64_t part_pitch, int n_slot
 			 uint64_t block_pitch, uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect,
 			 uint64_t *h_badmask, uint64_t chunk_bytes)
 {
-	if (!dec_args_ok(n_slots, navail, k, block_size, h_ids, h_avail))
+	if (!dec_args_ok(n_slots, navail, k, block_size, h_ids, h_avail, nstripes))
 		return -EINVAL;
 	if (!nkfs_gpu_ready())
 		return -EAGAIN;
@@ -1212,7 +1225,7 @@ int nkfs_nk8_decode_ragged_host(const uint8_t *h_parts, const uint64_t *h_part_o
 				uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect, uint64_t *h_badmask,
 				uint64_t chunk_bytes)
 {
-	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail))
+	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail, nstripes))
 		return -EINVAL;
 	if (!nkfs_gpu_ready())
 		return -EAGAIN;
@@ -1235,7 +1248,7 @@ int nkfs_nk8_decode_pages(const uint8_t *h_parts, const uint64_t *h_part_off, in
 			  uint32_t nstripes, int32_t *h_status, const uint64_t *h_expect, uint64_t *h_badmask,
 			  uint64_t chunk_bytes)
 {
-	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail))
+	if (!dec_args_ok(n_slots, navail, k, max_block_size, h_ids, h_avail, nstripes))
 		return -EINVAL;
 	if (!nkfs_gpu_ready())
 		return -EAGAIN;

@@ -61,6 +61,22 @@ def test_argument_validation_matches_reference():
     assert L.nk8_assemble_block(parts, ids, 1, 2, buf, 16) == -22
 
 
+def test_host_decode_rejects_missing_slots():
+    """The host-memory decode checks every offered slot exists before it
+    touches the GPU (the kernels index the stripe's id row with it): an
+    h_avail entry >= n_slots is -EINVAL, with or without a GPU."""
+    L = _lib.lib()
+    n, k, B, S = 4, 2, 4096, 3
+    parts = (C.c_uint8 * (S * n * 2048))()
+    blocks = (C.c_uint8 * (S * B))()
+    ids = (C.c_uint8 * (S * n))(*([1, 2, 3, 4] * S))
+    bad = (C.c_uint8 * (S * k))(0, 1, 2, 3, 1, 4)  # stripe 2 offers slot 4 of 4
+    assert L.nkfs_nk8_decode_host(parts, 2048, n, ids, bad, k, k, B, blocks, B, S, None, None, None, 0) == -22
+    ok = (C.c_uint8 * (S * k))(0, 1, 2, 3, 1, 3)
+    rc = L.nkfs_nk8_decode_host(parts, 2048, n, ids, ok, k, k, B, blocks, B, S, None, None, None, 0)
+    assert rc != -22
+
+
 @pytest.mark.skipif(has_gpu_device(), reason="checks the no-GPU behaviour")
 def test_no_gpu_fails_loudly():
     L = _lib.lib()
