@@ -83,11 +83,6 @@ __device__ inline u8 gf_mul(const GfLds &L, u8 a, u8 b)
     return (a && b) ? L.exp[L.log[a] + L.log[b]] : u8(0);
 }
 
-__device__ inline u8 gf_div(const GfLds &L, u8 a, u8 b)
-{
-    return (a && b) ? L.exp[L.log[a] + 255 - L.log[b]] : u8(0);
-}
-
 __device__ inline u64 shfl64(u64 v, int src)
 {
     u32 lo = __shfl(u32(v), src, 64);
@@ -234,6 +229,7 @@ __global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *ava
     __shared__ GfLds L;
     __shared__ u8 sid[256], sav[256], x[256], slot[256], M[2][260];
     __shared__ u8 q[64][256];  // one column's quotient per thread
+    __shared__ int firstoff[256];  // first offer of each id
     gf_stage(L, gft);
     const u32 s = blockIdx.x;
     const int tid = threadIdx.x;
@@ -242,10 +238,15 @@ __global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *ava
         sid[i] = ids[u64(s) * n_slots + i];
     for (int i = tid; i < navail; i += 64)
         sav[i] = avail[u64(s) * navail + i];
+    for (int i = tid; i < 256; i += 64)
+        firstoff[i] = 0x7FFFFFFF;
+    __syncthreads();
+    for (int c = tid; c < navail; c += 64)
+        atomicMin(&firstoff[sid[sav[c]]], c);
     __syncthreads();
     // first k offered slots with distinct ids, in offer order
-    // (crt/nk8.c:512-537): lane c keeps slot c unless an earlier offer has
-    // its id; a ballot prefix places the kept ones
+    // (crt/nk8.c:512-537): offer c is kept iff it is its id's first offer;
+    // a ballot prefix places the kept ones
     int h = 0;
     for (int base = 0; base < navail && h < k; base += 64) {
         const int c = base + tid;
@@ -254,9 +255,7 @@ __global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *ava
         if (c < navail) {
             sl = sav[c];
             id = sid[sl];
-            keep = true;
-            for (int d = 0; d < c; ++d)
-                keep &= sid[sav[d]] != id;
+            keep = firstoff[id] == c;
         }
         const u64 bal = __ballot(keep);
         const int pos = h + __popcll(bal & ((1ull << tid) - 1ull));
@@ -295,13 +294,27 @@ __global__ __launch_bounds__(64) void k_decode_prep(const u8 *ids, const u8 *ava
             qq = Mk[i] ^ gf_mul(L, xc, qq);
             qc[i - 1] = qq;
         }
-        // D = Q(x_c) = prod_{c' != c} (x_c + x_c')
-        u8 d = 0;
-        for (int i = k - 1; i >= 0; --i)
-            d = gf_mul(L, d, xc) ^ qc[i];
+        // D = Q(x_c) = prod_{c' != c} (x_c + x_c'): a sum of k - 1
+        // independent logs (the ids are distinct, so no factor is 0)
+        u32 lsum = 0;
+        for (int j = 0; j < k; ++j)
+            lsum += j == c ? 0u : u32(L.log[xc ^ x[j]]);
+        const u32 ld = lsum % 255u;
+        // W[c][i] = q_i / D, eight at a time: loads before stores
         u8 *row = wk + k + c * k;
-        for (int i = 0; i < k; ++i)
-            row[i] = gf_div(L, qc[i], d);
+        for (int i0 = 0; i0 < k; i0 += 8) {
+            u8 qv[8], ov[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                qv[t] = i0 + t < k ? qc[i0 + t] : u8(0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                ov[t] = qv[t] ? L.exp[L.log[qv[t]] + 255u - ld] : u8(0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (i0 + t < k)
+                    row[i0 + t] = ov[t];
+        }
     }
 }
 
