@@ -214,10 +214,16 @@ def check_rank_digests(gathered, n, expect_fn, samples=8):
     return len(gathered)
 
 
+_BARRIER_GPU = None  # the rank's GPU for RCCL barriers (set in main; None under gloo)
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
-        dist.barrier()
+        if _BARRIER_GPU is not None and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[_BARRIER_GPU])  # the communicator's own GPU, no guess by rank
+        else:
+            dist.barrier()
 
 
 # ----------------------------------------------------------------- timing
@@ -674,13 +680,15 @@ def main():
 
     # the rank's GPU is selected before the process group exists, so RCCL's
     # communicator binds to it (one process per GPU)
-    global _CDEV
+    global _CDEV, _BARRIER_GPU
     ngpu = max(1, torch.cuda.device_count())
     gpu = int(os.environ.get("LOCAL_RANK", "0")) % ngpu  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(gpu)
     rank, world, local = dist_setup(args.backend)
     if args.backend == "gloo":
         _CDEV = torch.device("cpu")
+    else:
+        _BARRIER_GPU = gpu
     device = torch.device("cuda", gpu)
     os.environ["NKFS_DEVICE"] = str(gpu)
     local = gpu
