@@ -218,6 +218,9 @@ def test_c2_full_batch_n4k2_4k(L, O):
     (512, 65536, 8, 5, 6),     # extra survivor offered
     (64, 70000, 255, 254, 254),
     (300, 777, 17, 16, 17),
+    (1024, 20480, 8, 5, 6),    # small batches of 4 KiB parts (plan + slice grid)
+    (300, 4096, 6, 3, 4),
+    (1025, 20480, 8, 5, 5),
 ])
 def test_uniform_shapes(L, O, S, B, n, k, keep):
     from nkfs_amd import batch
