@@ -369,14 +369,34 @@ def hbm_anchor(src, dst, stream):
     return _ANCHOR
 
 
-def with_box(roof, box):
-    """Attach the box's own stream ceiling to a roofline dict, and the
-    kernel's fraction of the guide's plain float4 copy measured on this box."""
+def anchor_mix(read_bytes, write_bytes):
+    """The HBM bound this box's anchor gives a kernel's read:write mix,
+    independent of the product's access shape: (r + w) / (r / read_GBps +
+    w / write_GBps) from the plain float4 read and write kernels
+    (hbm_anchor).  None before the anchor ran or for an empty mix."""
+    rd, wr = _ANCHOR.get("read_GBps"), _ANCHOR.get("write_GBps")
+    if not rd or not wr or read_bytes + write_bytes <= 0:
+        return None
+    return (read_bytes + write_bytes) / (read_bytes / rd + write_bytes / wr)
+
+
+def with_box(roof, box, rw=None):
+    """Attach the box's own ceilings to a roofline dict: `box_stream` (the
+    kernel's read:write mix through k_mix, the product's access shape; its
+    spread between buffers of one process is a few %), the
+    fraction of the guide's plain float4 copy, and -- rw = (read bytes,
+    write bytes) of one launch -- `frac_of_anchor_mix`, the fraction of the
+    bound the anchor's read and write rates give that mix (anchor_mix)."""
     if box:
         roof["box_stream"] = box
         roof["frac_of_box_stream"] = round(roof["achieved"] / box["GBps"], 4)
     if _ANCHOR.get("copy_GBps"):
         roof["frac_of_anchor_copy"] = round(roof["achieved"] / _ANCHOR["copy_GBps"], 4)
+    if rw is not None:
+        bound = anchor_mix(*rw)
+        if bound:
+            roof["anchor_mix_GBps"] = round(bound, 1)
+            roof["frac_of_anchor_mix"] = round(roof["achieved"] / bound, 4)
     return roof
 
 
@@ -424,7 +444,7 @@ def uniform_result(name, args, rank, world, device, S, B, n, k, desc, strong_tot
     user_bytes = total_stripes * B * steps
     dec = with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
                     "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4), "us_per_launch": round(dec_s * 1e6, 2),
-                    "bytes_per_launch": dec_bytes}, box_dec)
+                    "bytes_per_launch": dec_bytes}, box_dec, (S * k * ps, S * B))
     res = {
         "value": round(user_bytes / elapsed / 2**30, 3), "unit": "GiB/s", "steps": steps,
         "ms_per_step": round(elapsed / steps * 1e3, 4), "timed_ms": round(elapsed * 1e3, 1),
@@ -433,7 +453,7 @@ def uniform_result(name, args, rank, world, device, S, B, n, k, desc, strong_tot
                    "erased_per_stripe": n - k, "parallelism": f"stripe-partition x{world}",
                    "stripes_all_gpus": total_stripes},
         "roofline": with_box(roofline("nkfs_nk8_encode (encode + XXH64 per part)", enc_bytes, enc_s,
-                                      pmc_traffic(name, S, world)), box_enc),
+                                      pmc_traffic(name, S, world)), box_enc, (S * B, S * n * ps + 8 * S * n)),
         "decode": dec,
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
         "per_rank": rank_spread(enc_s, dec_s, device),
@@ -620,10 +640,11 @@ def run_ragged(args, rank, world, device, steps):
                    "parallelism": f"stripe-partition x{world} (byte-balanced ranges)"},
         "scaling": "weak",
         "roofline": with_box(roofline("nkfs_nk8_encode_ragged (encode + XXH64 per part)", enc_bytes, enc_s,
-                                      pmc_traffic("c5", S, world)), box_enc),
+                                      pmc_traffic("c5", S, world)), box_enc, (user, n * sum(ps) + 8 * n * S)),
         "decode": with_box({"achieved": round(dec_bytes / dec_s / 1e9, 1), "achieved_GBps": round(dec_bytes / dec_s / 1e9, 1),
                             "frac": round(dec_bytes / dec_s / 1e9 / HBM_PEAK_GBS, 4),
-                            "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes}, box_dec),
+                            "us_per_launch": round(dec_s * 1e6, 2), "bytes_per_launch": dec_bytes}, box_dec,
+                           (k * sum(ps), user)),
         "verified": ok, "verified_ranks": ranks_ok, "digest_xor_per_rank": [f"{x:016x}" for x in gathered],
         "per_rank": rank_spread(enc_s, dec_s, device),
     }

@@ -58,7 +58,7 @@ struct Shape {
     int per_cu;
 };
 
-Shape occupancy_shape(const void *kern, int target)
+[[maybe_unused]] Shape occupancy_shape(const void *kern, int target)
 {
     static std::mutex mu;
     static std::map<std::pair<const void *, int>, Shape> cache;
@@ -81,12 +81,12 @@ Shape occupancy_shape(const void *kern, int target)
     return sh;
 }
 
-u32 part_size_of_host(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
+[[maybe_unused]] u32 part_size_of_host(u32 B, int k) { return B / u32(k) + ((B % u32(k)) ? 1u : 0u); }
 
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 // bit-serial GF(2^8)/0x11B product (crt/nk8.c:54-74) in registers
-__device__ inline u32 gfm_bits(u32 a, u32 b)
+[[maybe_unused]] __device__ inline u32 gfm_bits(u32 a, u32 b)
 {
     u32 r = 0;
 #pragma unroll
@@ -136,10 +136,12 @@ __host__ __device__ inline bool walk_offsets_fit(u64 block_size, u64 part_span, 
     return block_size + 2048u * 8u <= 0x7FFFFFFFull && part_span <= 0x7FFFFFFFull && nstripes * n * 8u <= 0x7FFFFFFFull;
 }
 
+#ifndef NKFS_WALK_K
 extern "C" int nkfs_walk_offsets_fit(uint64_t block_size, uint64_t part_span, uint64_t nstripes, uint64_t n)
 {
     return walk_offsets_fit(block_size, part_span, nstripes, n);
 }
+#endif
 
 // Buffer offset `off` (< 2^31) when `live`, else past every num_records
 // (the load reads 0 / the store is dropped), as plain
@@ -843,6 +845,7 @@ __global__ __launch_bounds__(64) void k_decode_slice(nkfs_geom g, int n_slots, c
     }
 }
 
+#ifndef NKFS_WALK_K
 // Exclusive prefix of the slices per stripe of a ragged batch in processing
 // order (g.order applied): sfirst[0..nstripes], *stotal = sfirst[nstripes].
 // One workgroup; every thread sums a contiguous run of stripes.
@@ -904,6 +907,8 @@ __global__ __launch_bounds__(256) void k_slice_map(const u32 *sfirst, u32 nstrip
         smap[a + j] = (u64(p) << 32) | j;
 }
 
+#endif  // !NKFS_WALK_K
+
 // ----------------------------------------------------------------- launchers
 
 template <int K, int E, int U, int P, bool HASH, bool NIB>
@@ -932,31 +937,56 @@ static void launch_walk_kk(hipStream_t st, const nkfs_geom &g, const u8 *ids, u6
                        per_wave);
 }
 
-template <int E, int U, int P, bool HASH, bool NIB>
-static int launch_walk_kp(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
-{
-    switch (k) {
-    case 2: launch_walk_kk<2, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 3: launch_walk_kk<3, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 4: launch_walk_kk<4, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 5: launch_walk_kk<5, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 6: launch_walk_kk<6, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 7: launch_walk_kk<7, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    case 8: launch_walk_kk<8, E, U, P, HASH, NIB>(st, g, ids, dig, waves, cus); return 0;
-    default: return -ENOSYS;
-    }
-}
-
 // prefetch depth 2 only for the byte-table forms (nibble tables keep P = 1)
-template <int E, int U, bool HASH, bool NIB>
-static int launch_walk_k(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
+template <int K, int E, int U, bool HASH, bool NIB>
+static void launch_walk_k(hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, int waves, int cus)
 {
     if constexpr (!NIB)
         if (nkfs_tune_now().enc_prefetch >= 2)
-            return launch_walk_kp<E, U, 2, HASH, NIB>(k, st, g, ids, dig, waves, cus);
-    return launch_walk_kp<E, U, 1, HASH, NIB>(k, st, g, ids, dig, waves, cus);
+            return launch_walk_kk<K, E, U, 2, HASH, NIB>(st, g, ids, dig, waves, cus);
+    launch_walk_kk<K, E, U, 1, HASH, NIB>(st, g, ids, dig, waves, cus);
 }
 
+// Per-k entry points.  The Makefile compiles this file once per k
+// (-DNKFS_WALK_K=2..8: that k's kernels and these two functions) and once
+// without (the dispatchers below): the kernels of all seven k in one
+// translation unit took ~400 s to compile, one k takes a seventh of it.
+namespace nkfs {
+template <int K>
+void walk_encode_k(const nkfs_geom &g, const u8 *ids, u64 *dig, int units, int nib, int waves, int cus,
+                   hipStream_t st)
+{
+    const bool h = dig != nullptr;
+    if (g.n <= 4) {
+        if (units == 2)
+            h ? launch_walk_k<K, 4, 2, true, false>(st, g, ids, dig, waves, cus)
+              : launch_walk_k<K, 4, 2, false, false>(st, g, ids, dig, waves, cus);
+        else
+            h ? launch_walk_k<K, 4, 1, true, false>(st, g, ids, dig, waves, cus)
+              : launch_walk_k<K, 4, 1, false, false>(st, g, ids, dig, waves, cus);
+    } else if (nib) {
+        h ? launch_walk_k<K, 8, 1, true, true>(st, g, ids, dig, waves, cus)
+          : launch_walk_k<K, 8, 1, false, true>(st, g, ids, dig, waves, cus);
+    } else {
+        h ? launch_walk_k<K, 8, 1, true, false>(st, g, ids, dig, waves, cus)
+          : launch_walk_k<K, 8, 1, false, false>(st, g, ids, dig, waves, cus);
+    }
+}
+
+#ifdef NKFS_WALK_K
+template void walk_encode_k<NKFS_WALK_K>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+#else
+extern template void walk_encode_k<2>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<3>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<4>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<5>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<6>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<7>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+extern template void walk_encode_k<8>(const nkfs_geom &, const u8 *, u64 *, int, int, int, int, hipStream_t);
+#endif
+}  // namespace nkfs
+
+#ifndef NKFS_WALK_K
 // Walk encoder for n <= 8, k <= 8 (uniform or ragged; g->order honoured).
 // units: 1,024-row units per chunk.  -ENOSYS where the buffer offsets of a
 // stripe would not fit 31 bits (the generic kernels take those).
@@ -973,23 +1003,19 @@ extern "C" int nkfs_walk_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // setting bit 31, which lands past num_records only for offsets below 2^31
     if (!walk_offsets_fit(g->block_size, u64(g->n) * pitch, g->nstripes, g->n))
         return -ENOSYS;
-    const bool h = digests != nullptr;
-    int rc;
-    if (g->n <= 4)
-        rc = units == 2 ? (h ? launch_walk_k<4, 2, true, false>(g->k, st, *g, ids, digests, waves, cus)
-                             : launch_walk_k<4, 2, false, false>(g->k, st, *g, ids, digests, waves, cus))
-                        : (h ? launch_walk_k<4, 1, true, false>(g->k, st, *g, ids, digests, waves, cus)
-                             : launch_walk_k<4, 1, false, false>(g->k, st, *g, ids, digests, waves, cus));
-    else if (nib)
-        rc = h ? launch_walk_k<8, 1, true, true>(g->k, st, *g, ids, digests, waves, cus)
-               : launch_walk_k<8, 1, false, true>(g->k, st, *g, ids, digests, waves, cus);
-    else
-        rc = h ? launch_walk_k<8, 1, true, false>(g->k, st, *g, ids, digests, waves, cus)
-               : launch_walk_k<8, 1, false, false>(g->k, st, *g, ids, digests, waves, cus);
-    if (rc)
-        return rc;
+    switch (g->k) {
+    case 2: walk_encode_k<2>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 3: walk_encode_k<3>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 4: walk_encode_k<4>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 5: walk_encode_k<5>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 6: walk_encode_k<6>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 7: walk_encode_k<7>(*g, ids, digests, units, nib, waves, cus, st); break;
+    case 8: walk_encode_k<8>(*g, ids, digests, units, nib, waves, cus, st); break;
+    default: return -ENOSYS;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+#endif  // !NKFS_WALK_K
 
 // uniform: one wave per (stripe, slice); ragged: a persistent grid of the
 // resident waves over the scanned slice list
@@ -1021,6 +1047,39 @@ static void launch_slice_u(int units, hipStream_t st, const nkfs_geom &g, int n_
         launch_slice<K, E, 1, XP>(st, g, n_slots, plan, slices, waves, smap, stotal, cus);
 }
 
+namespace nkfs {
+template <int K>
+void slice_decode_k(const nkfs_geom &g, int n_slots, const u8 *ids, const u8 *avail, int navail, u8 *plan,
+                    int32_t *status, const GfTables *gft, int units, u32 slices, int waves, const u64 *smap,
+                    const u32 *stotal, int cus, hipStream_t st)
+{
+    const dim3 pgrid(u32((u64(g.nstripes) * u64(K) + 255) / 256));  // k_decode_plan: k lanes per stripe
+    hipLaunchKernelGGL((k_decode_plan<K>), pgrid, dim3(256), 0, st, ids, avail, n_slots, navail, g.nstripes, plan,
+                       status, gft);
+    launch_slice_u<K, (K <= 4 ? 4 : 8)>(units, st, g, n_slots, plan, slices, waves, smap, stotal, cus);
+}
+
+#ifdef NKFS_WALK_K
+template void slice_decode_k<NKFS_WALK_K>(const nkfs_geom &, int, const u8 *, const u8 *, int, u8 *, int32_t *,
+                                          const GfTables *, int, u32, int, const u64 *, const u32 *, int,
+                                          hipStream_t);
+#else
+#define NKFS_EXT(KK)                                                                                            \
+    extern template void slice_decode_k<KK>(const nkfs_geom &, int, const u8 *, const u8 *, int, u8 *, int32_t *, \
+                                            const GfTables *, int, u32, int, const u64 *, const u32 *, int,     \
+                                            hipStream_t);
+NKFS_EXT(2)
+NKFS_EXT(3)
+NKFS_EXT(4)
+NKFS_EXT(5)
+NKFS_EXT(6)
+NKFS_EXT(7)
+NKFS_EXT(8)
+#undef NKFS_EXT
+#endif
+}  // namespace nkfs
+
+#ifndef NKFS_WALK_K
 // Slice decoder, k <= 8: plan kernel (selection + inverse per stripe into
 // `work`, nkfs_decode_work_bytes layout) then one-shot slice waves; a ragged
 // batch (g->order honoured) first scans its slice counts into stream-ordered
@@ -1036,7 +1095,6 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         return 0;
     u8 *plan = static_cast<u8 *>(work);
     const GfTables *gft = static_cast<const GfTables *>(gf);
-    const dim3 pgrid(u32((u64(g->nstripes) * u64(g->k) + 255) / 256));  // k_decode_plan: k lanes per stripe
     const u32 ps = part_size_of_host(g->block_size, g->k);  // ragged: the bound on block sizes
     units = units >= 4 ? 4 : units >= 2 ? 2 : 1;
     // a stripe that fits in fewer units takes one wave of just those
@@ -1063,20 +1121,13 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
     const u32 *stotal = scan ? scan + g->nstripes + 1 : nullptr;
     int rc = 0;
     switch (g->k) {
-#define NKFS_DK(KK, EE)                                                                                          \
-    case KK:                                                                                                     \
-        hipLaunchKernelGGL((k_decode_plan<KK>), pgrid, dim3(256), 0, st, ids, avail, n_slots, navail, g->nstripes, \
-                           plan, status, gft);                                                                   \
-        launch_slice_u<KK, EE>(units, st, *g, n_slots, plan, slices, waves, smap, stotal, cus);                  \
-        break;
-        NKFS_DK(2, 4)
-        NKFS_DK(3, 4)
-        NKFS_DK(4, 4)
-        NKFS_DK(5, 8)
-        NKFS_DK(6, 8)
-        NKFS_DK(7, 8)
-        NKFS_DK(8, 8)
-#undef NKFS_DK
+    case 2: slice_decode_k<2>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 3: slice_decode_k<3>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 4: slice_decode_k<4>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 5: slice_decode_k<5>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 6: slice_decode_k<6>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 7: slice_decode_k<7>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
+    case 8: slice_decode_k<8>(*g, n_slots, ids, avail, navail, plan, status, gft, units, slices, waves, smap, stotal, cus, st); break;
     default:
         rc = -ENOSYS;
     }
@@ -1087,3 +1138,4 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const uint8_t 
         return rc;
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+#endif  // !NKFS_WALK_K

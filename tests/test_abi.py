@@ -205,3 +205,26 @@ def test_pipeline_plan_rejects_bad_geometry():
     boff, poff = _ragged(sizes, 4, 2, 0, 0)
     boff[1] -= 1  # blocks overlap
     assert _plan(0, boff, sizes, 4, 2, 4, poff, 0, 0)[0] == -22
+
+
+@pytest.mark.timeout(900)
+def test_debug_bounds_build_compiles():
+    """the debug-bounds build (make DEBUG_BOUNDS=1: the
+    ragged walk encoder's and slice decoder's range reports)
+    compiles from the current sources and exports the product's ABI, so
+    tests/test_gpu_debug_bounds.py can load it on the GPU box.  Incremental:
+    build() normally made it already."""
+    import os
+    csrc = os.path.join(os.path.dirname(_lib.LIB_PATH), "..", "csrc")
+    r = subprocess.run(["make", "-C", csrc, "DEBUG_BOUNDS=1", "-j", str(min(8, os.cpu_count() or 2))],
+                       capture_output=True, text=True, timeout=880)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    dbg = os.path.join(os.path.dirname(_lib.LIB_PATH), "debug", "libnkfs_crt.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", dbg], capture_output=True, text=True, check=True)
+    syms = {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+    assert syms == exported()
+    # the range checks are really compiled in: their report format is in the device code
+    strings = subprocess.run(["strings", os.path.join(csrc, "..", "build", "debug", "nk8_walk_k5.o")],
+                             capture_output=True, text=True, check=True).stdout
+    obj = subprocess.run(["grep", "-c", "nkfs bounds"], input=strings, capture_output=True, text=True)
+    assert int(obj.stdout.strip() or 0) >= 1

@@ -17,7 +17,8 @@ import bench  # noqa: E402
 
 def main():
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29531", rank=0, world_size=1)
+    port = int(os.environ.get("NKFS_SMOKE_PORT", "29531"))
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     bench._BARRIER_GPU = 0
     dev = torch.device("cuda", 0)
     bench.barrier()
