@@ -401,11 +401,11 @@ XXH_errorcode XXH64_update(XXH64_state_t *state_in, const void *input, size_t le
 static int finish(struct xstate *s, uint64_t *out)
 {
 	for (;;) {
-		int stale;
-		struct xslot *sl = slot_of(s, &stale);
-		if (stale)
-			return -EINVAL;
-		if (!sl) { /* nothing on the GPU: merge + tail + avalanche in one launch */
+		const uint32_t pend = __atomic_load_n(&s->pend, __ATOMIC_ACQUIRE);
+		if (pend == PEND_POISON)
+			return -EIO;
+		if ((pend & 0xFFFF0000u) != PEND_MAGIC) {
+			/* nothing on the GPU: merge + tail + avalanche in one launch */
 			struct xh h;
 			uint64_t v0[4];
 			memcpy(v0, s->v, 32);
@@ -415,14 +415,25 @@ static int finish(struct xstate *s, uint64_t *out)
 			xh_end(&h);
 			return err;
 		}
+		const uint32_t i = pend & 0xFFFFu;
+		if (i >= NSLOT)
+			return -EINVAL;
+		struct xslot *sl = &g_slot[i];
+		/* everything below under the slot's mutex: a concurrent digest that
+		 * completes this message writes the accumulators into s->v and then
+		 * clears s->pend while holding it, so the pair is never seen half
+		 * written (pend still set, v[0] no longer the token) */
 		pthread_mutex_lock(&sl->mu);
-		const uint32_t pend = __atomic_load_n(&s->pend, __ATOMIC_ACQUIRE);
-		pthread_mutex_lock(&g_slot_lock);
-		const int mine = pend == (PEND_MAGIC | (uint32_t)(sl - g_slot)) && sl->used && sl->token == s->v[0];
-		pthread_mutex_unlock(&g_slot_lock);
-		if (!mine) { /* another digest completed it meanwhile: look again */
-			pthread_mutex_unlock(&sl->mu);
+		if (__atomic_load_n(&s->pend, __ATOMIC_ACQUIRE) != pend) {
+			pthread_mutex_unlock(&sl->mu); /* completed meanwhile: look again */
 			continue;
+		}
+		pthread_mutex_lock(&g_slot_lock);
+		const int mine = sl->used && sl->token == s->v[0];
+		pthread_mutex_unlock(&g_slot_lock);
+		if (!mine) { /* a byte copy of a state whose message is gone */
+			pthread_mutex_unlock(&sl->mu);
+			return -EINVAL;
 		}
 		uint64_t v[4];
 		int err = xh_complete(&sl->h, NKFS_XXH_FINISH | NKFS_XXH_EMIT, s, out, v);
