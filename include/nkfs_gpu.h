@@ -63,8 +63,10 @@ int nkfs_gpu_get_devices(int *devices, int max);
  * (a hash wave per workgroup; the default for k <= 16 batches that fill the
  * chip); NKFS_ENC_GENERIC: thread-per-row kernel; NKFS_ENC_BIG:
  * column-chunked encoder (any k; the default for k > 16) */
+/* NKFS_ENC_WSP: persistent warp-specialised encoder (n <= 8, k <= 8, with
+ * digests; ragged batches in size order from a device-wide group counter) */
 enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG,
-       NKFS_ENC_WIDE_WS };
+       NKFS_ENC_WIDE_WS, NKFS_ENC_WSP };
 /* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16);
  * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16);
  * NKFS_DEC_RUN: run decoder (k <= 8: persistent waves, each walking one
@@ -98,6 +100,9 @@ struct nkfs_tune {
 	                         general kernels + a hash pass instead of one wave per stripe (0..63) */
 	int enc_ws_hash_waves; /* warp-specialised encoder, n > 4 with 4 encoder waves: hash waves per workgroup
 	                          (0 auto: 2 from 1,024 stripes on; 1; 2) */
+	int enc_persist;      /* n > 4 with digests: the persistent warp-specialised encoder (NKFS_ENC_WSP) where the
+	                         automatic choice is the warp-specialised grid (uniform) or the walk encoder (ragged);
+	                         0 = off, 1 = on */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

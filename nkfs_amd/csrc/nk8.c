@@ -143,7 +143,7 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 		uint8_t *h = hv;
 		memcpy(h, block, B);
 		memcpy(h + off_ids, ids, (size_t)n);
-		struct nkfs_geom zg = { h, round16(B), B, NULL, NULL, h + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
+		struct nkfs_geom zg = { h, round16(B), B, NULL, NULL, h + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 		if ((err = nkfs_launch_encode(&zg, h + off_ids, NULL, nkfs_gf(), c->stream)) ||
 		    (err = nkfs_ctx_wait(c, B >= NKFS_SPIN_MIN)))
 			goto out;
@@ -159,7 +159,7 @@ static int gpu_split(const uint8_t *block, uint32_t B, int n, int k, const uint8
 	memcpy(h, block, B);
 	memcpy(h + off_ids, ids, (size_t)n);
 	HIPGO(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
-	struct nkfs_geom g = { d, round16(B), B, NULL, NULL, d + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
+	struct nkfs_geom g = { d, round16(B), B, NULL, NULL, d + off_parts, pitch, NULL, 1, n, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	if ((err = nkfs_launch_encode(&g, d + off_ids, NULL, nkfs_gf(), c->stream)))
 		goto out;
 	HIPGO(hipMemcpyAsync(h, d + off_parts, parts_bytes, hipMemcpyDeviceToHost, c->stream));
@@ -253,7 +253,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 			h[off_avail + c2] = (uint8_t)c2;
 		}
 		struct nkfs_geom zg = { h + off_block, round16(block_size), block_size, NULL, NULL, h + off_parts, pitch,
-					NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0 };
+					NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 		if ((err = nkfs_launch_decode(&zg, k, h + off_ids, h + off_avail, k, h + off_work,
 					      (int32_t *)(h + off_status), nkfs_gf(), c->stream, NULL, NULL)) ||
 		    (err = nkfs_ctx_wait(c, block_size >= NKFS_SPIN_MIN)))
@@ -276,7 +276,7 @@ int nk8_assemble_block(uint8_t **parts, uint8_t *ids, int n, int k, uint8_t *blo
 	}
 	HIPGO(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
 	struct nkfs_geom g = { d + off_block, round16(block_size), block_size, NULL, NULL, d + off_parts, pitch,
-			       NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0 };
+			       NULL, 1, k, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	if ((err = nkfs_launch_decode(&g, k, d + off_ids, d + off_avail, k, d + off_work,
 				      (int32_t *)(d + off_status), nkfs_gf(), c->stream, NULL, NULL)))
 		goto out;

@@ -477,6 +477,8 @@ __global__ __launch_bounds__(1024) void k_order_by_size(const u32 *sizes, u32 co
         if (i < count)
             perm[pos] = i;
     }
+    if (t == 0)
+        perm[count] = 0;  // the launcher's group counter for a persistent grid over the order
 }
 
 // ---------------------------------------------------------- synthetic
@@ -626,7 +628,7 @@ extern "C" hipMemPool_t nkfs_private_pool(hipStream_t st)
 
 extern "C" uint64_t nkfs_ragged_scratch_bytes(uint32_t nstripes, uint64_t sum_units)
 {
-    const u64 perm = (u64(nstripes) * 4 + 255) & ~u64(255);
+    const u64 perm = ((u64(nstripes) + 1) * 4 + 255) & ~u64(255);  // + the persistent launches' group counter
     const u64 head = ((u64(nstripes) + 2) * 4 + 15) & ~u64(15);
     return perm + ((head + sum_units * 8 + 255) & ~u64(255));
 }
@@ -642,13 +644,16 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
     if (!g->block_sizes || g->order || !nkfs_tune_now().size_order || g->nstripes > ORDER_MAXP * 1024u)
         return -ENOSYS;  // (k_order_by_size: ORDER_MAXP stripes per thread)
     Scratch sc;
-    u32 *perm = static_cast<u32 *>(sc.take(g, u64(g->nstripes) * sizeof(u32), st));
+    // the permutation, then one zeroed word: the group counter of a
+    // persistent launch over the order (nk8_wsp.hip)
+    u32 *perm = static_cast<u32 *>(sc.take(g, (u64(g->nstripes) + 1) * sizeof(u32), st));
     if (!perm)
         return -ENOSYS;
     hipLaunchKernelGGL(k_order_by_size, dim3(1), dim3(1024), 0, st, g->block_sizes, g->nstripes, g->k, perm);
     int rc = launch_ok();
     nkfs_geom g2 = *g;
     g2.order = perm;
+    g2.queue = perm + g->nstripes;
     sc.rest(&g2);
     if (!rc)
         rc = launch(&g2);
@@ -658,6 +663,7 @@ static int with_size_order(const nkfs_geom *g, hipStream_t st, F launch)
 
 extern "C" int nkfs_walk_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, int units, int nib, int waves,
                                 int cus, hipStream_t st);
+extern "C" int nkfs_wsp_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool nt, hipStream_t st);
 extern "C" int nkfs_wide_encode(const nkfs_geom *g, const uint8_t *ids, int cus, hipStream_t st);
 extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st);
 extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
@@ -712,9 +718,21 @@ static int walk_by_rule(const nkfs_geom *g, const u64 *digests)
 static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStream_t st)
 {
     const nkfs_tune t = nkfs_tune_now();
-    const int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
-                     : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
-                                                                  : NKFS_ENC_AUTO;
+    int kern = t.enc_kernel != NKFS_ENC_AUTO ? t.enc_kernel
+               : g->block_sizes || walk_by_rule(g, digests) ? NKFS_ENC_WALK
+                                                            : NKFS_ENC_AUTO;
+    // enc_persist: n > 4 batches with digests take the persistent
+    // warp-specialised encoder where the choice above is the walk encoder on
+    // a ragged batch or the warp-specialised grid on a uniform one
+    if (t.enc_kernel == NKFS_ENC_AUTO && t.enc_persist && digests && g->n > 4 &&
+        (g->block_sizes ? kern == NKFS_ENC_WALK : kern == NKFS_ENC_AUTO))
+        kern = NKFS_ENC_WSP;
+    if (kern == NKFS_ENC_WSP) {
+        const int rc = nkfs_wsp_encode(g, ids, digests, false, st);
+        if (rc != -ENOSYS)
+            return rc;
+        kern = g->block_sizes ? NKFS_ENC_WALK : NKFS_ENC_AUTO;
+    }
     if (kern == NKFS_ENC_WALK && g->block_sizes && digests && g->n > 4 && t.enc_ragged_split &&
         !g->part_min && !g->part_max) {
         // ragged n > 4: stripes with parts of at least enc_ragged_split bytes

@@ -47,6 +47,9 @@ struct nkfs_geom {
 	 * asserts (make DEBUG_BOUNDS=1); 0 = unknown. */
 	uint64_t blocks_bytes;
 	uint64_t parts_bytes;
+	/* optional zeroed device word: the group counter of a persistent launch
+	 * over g.order (k_order_by_size zeroes it; with_size_order sets it) */
+	uint32_t *queue;
 };
 
 /* Scratch bytes the launchers take from nkfs_geom.scratch for a ragged

@@ -67,6 +67,7 @@ static struct nkfs_tune g_tune = {
 	.enc_ws_waves = 4,
 	.enc_few_max = 63,
 	.enc_ws_hash_waves = 0, /* auto: 2 from 1,024 stripes (profiles/r04/seam_ws2.txt) */
+	.enc_persist = 0,
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
 
@@ -81,7 +82,7 @@ void nkfs_tune_get(struct nkfs_tune *t)
 
 int nkfs_tune_set(const struct nkfs_tune *t)
 {
-	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WIDE_WS || t->dec_kernel < NKFS_DEC_AUTO ||
+	if (!t || t->enc_kernel < NKFS_ENC_AUTO || t->enc_kernel > NKFS_ENC_WSP || t->dec_kernel < NKFS_DEC_AUTO ||
 	    t->dec_kernel > NKFS_DEC_PAIR || t->enc_waves_per_cu < 1 || t->enc_waves_per_cu > 32 ||
 	    t->dec_waves_per_cu < 1 || t->dec_waves_per_cu > 32 ||
 	    (t->dec_units != 1 && t->dec_units != 2 && t->dec_units != 4) || t->enc_nib < -1 || t->enc_nib > 1 ||
@@ -95,7 +96,8 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
 	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0 ||
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||
-	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2)
+	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2 ||
+	    (t->enc_persist != 0 && t->enc_persist != 1))
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;
@@ -542,7 +544,7 @@ int nkfs_nk8_encode(const uint8_t *d_blocks, uint64_t block_pitch, uint32_t bloc
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, d_parts, part_pitch, NULL,
-			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
+			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
@@ -562,7 +564,7 @@ int nkfs_nk8_encode_ragged(const uint8_t *d_blocks, const uint64_t *d_block_off,
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, d_parts, 0, d_part_off,
-			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0 };
+			       nstripes, n, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	return nkfs_launch_encode(&g, d_ids, d_digests, gf, stream);
 }
 
@@ -589,7 +591,7 @@ static int decode_common(const uint8_t *d_parts, uint64_t part_pitch, int n_slot
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, block_pitch, block_size, NULL, NULL, (uint8_t *)d_parts, part_pitch, NULL,
-			       nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0 };
+			       nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
 				  d_badmask);
 }
@@ -620,7 +622,7 @@ static int decode_ragged_common(const uint8_t *d_parts, const uint64_t *d_part_o
 	if (!gf)
 		return -ENODEV;
 	struct nkfs_geom g = { d_blocks, 0, max_block_size, d_block_off, d_block_size, (uint8_t *)d_parts, 0,
-			       d_part_off, nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0 };
+			       d_part_off, nstripes, n_slots, k, NULL, 0, 0, NULL, 0, 0, 0, NULL };
 	return nkfs_launch_decode(&g, n_slots, d_ids, d_avail, navail, d_work, d_status, gf, stream, d_expect,
 				  d_badmask);
 }
