@@ -101,8 +101,11 @@ struct nkfs_tune {
 	int enc_ws_hash_waves; /* warp-specialised encoder, n > 4 with 4 encoder waves: hash waves per workgroup
 	                          (0 auto: 2 from 1,024 stripes on; 1; 2) */
 	int enc_persist;      /* n > 4 with digests: the persistent warp-specialised encoder (NKFS_ENC_WSP) where the
-	                         automatic choice is the warp-specialised grid (uniform) or the walk encoder (ragged);
-	                         0 = off, 1 = on */
+	                         automatic choice is the walk encoder (ragged batches: 1, the default) or also the
+	                         warp-specialised grid (uniform batches: 2); 0 = off */
+	int dec_bign;         /* k > 8 decode on the replicated-table decoder (nk8_bign.hip): -1 = off (survivor-table /
+	                         column-chunked decoders), 0 = byte tables, 1 = byte tables x 2 replicas, 2 = nibble
+	                         tables x 16 replicas (every lookup in its lane's own bank slot) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

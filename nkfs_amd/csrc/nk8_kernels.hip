@@ -669,6 +669,8 @@ extern "C" int nkfs_wide_ws_encode(const nkfs_geom *g, const uint8_t *ids, uint6
 extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, const void *gf,
                                hipStream_t st);
 extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st);
+extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int mode,
+                                hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
@@ -723,9 +725,11 @@ static int fast_encode(const nkfs_geom *g, const u8 *ids, u64 *digests, hipStrea
                                                             : NKFS_ENC_AUTO;
     // enc_persist: n > 4 batches with digests take the persistent
     // warp-specialised encoder where the choice above is the walk encoder on
-    // a ragged batch or the warp-specialised grid on a uniform one
+    // a ragged batch (1, the default: C5 4,839 -> 5,051 GB/s) or also the
+    // warp-specialised grid on a uniform one (2: C3 5,109 -> 5,064, C4 5,148
+    // -> 5,144; profiles/r05/ab_wsp.txt)
     if (t.enc_kernel == NKFS_ENC_AUTO && t.enc_persist && digests && g->n > 4 &&
-        (g->block_sizes ? kern == NKFS_ENC_WALK : kern == NKFS_ENC_AUTO))
+        (g->block_sizes ? kern == NKFS_ENC_WALK : t.enc_persist == 2 && kern == NKFS_ENC_AUTO))
         kern = NKFS_ENC_WSP;
     if (kern == NKFS_ENC_WSP) {
         const int rc = nkfs_wsp_encode(g, ids, digests, false, st);
@@ -907,9 +911,15 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         return rc;
     // k <= 16: survivor tables of 16-byte products (nk8_wide.hip); beyond:
     // 16-column chunks (nk8_big.hip); pinned GENERIC: thread per row
-    rc = t.dec_kernel == NKFS_DEC_GENERIC || t.dec_kernel == NKFS_DEC_BIG
-             ? -ENOSYS
-             : nkfs_wide_decode(g, (const u8 *)work, status, nkfs_cu_count(), st);
+    // dec_bign >= 0: the replicated-table decoder for every k > 8 (unless a
+    // family is pinned)
+    rc = -ENOSYS;
+    if (t.dec_bign >= 0 && (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG))
+        rc = nkfs_bign_decode(g, (const u8 *)work, status, t.dec_bign, st);
+    if (rc == -ENOSYS)
+        rc = t.dec_kernel == NKFS_DEC_GENERIC || t.dec_kernel == NKFS_DEC_BIG
+                 ? -ENOSYS
+                 : nkfs_wide_decode(g, (const u8 *)work, status, nkfs_cu_count(), st);
     if (rc == -ENOSYS && t.dec_kernel != NKFS_DEC_GENERIC)
         rc = nkfs_big_decode(g, (const u8 *)work, status, st);
     if (rc == -ENOSYS) {

@@ -42,6 +42,7 @@
 
 #include "nk8_dev.h"
 #include "nkfs_internal.h"
+#include "scratch.h"
 #include "xxh64_dev.h"
 
 using namespace nkfs;
@@ -292,8 +293,10 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
         // load pointer: task t+PF
         u32 jl = 0, cl = 0, nchl = ring_nch[0];
         Geo gl = geo(0);
-        auto load_task = [&](u32 (&x)[4 * K]) {
-            // chunk cl of group jl (if any), then advance the pointer
+        // issue the loads of the task at the load pointer (no LDS access:
+        // the pointer is advanced at the top of the next step, so the ring
+        // reads never sit between the table lookups and their uses)
+        auto load_issue = [&](u32 (&x)[4 * K]) {
             if (nchl == WSP_END)
                 return;
             const u32 r0 = cl * CR + rbase;
@@ -322,6 +325,10 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
                     }
                 }
             }
+        };
+        auto load_advance = [&]() {
+            if (nchl == WSP_END)
+                return;
             if (++cl >= nchl) {
                 ++jl;
                 cl = 0;
@@ -333,14 +340,18 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
 
         u32 d[PF][4 * K];
 #pragma unroll
-        for (int p = 0; p < PF; ++p)
-            load_task(d[p]);
+        for (int p = 0; p < PF; ++p) {
+            load_issue(d[p]);
+            load_advance();
+        }
 
         u8 *mytbl = tbl + e * (K - 1) * TB;
         u32 j = 0, c = 0, nchj = ring_nch[0];
         Geo ge = geo(0);
 
         auto chunk = [&](u32 (&x)[4 * K], u32 t) {
+            if (t > 0)
+                load_advance();  // to task t + PF (issued at the end of this step's lookups)
             if (c == 0 && ge.live) {
                 // a new group: this wave's stripe's tables (the previous
                 // group's last lookups are behind us in program order)
@@ -399,7 +410,7 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
                     if constexpr (K * W > 8)
                         asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(out[0][q]));
                 }
-                load_task(x);  // task t + PF, in flight under what follows
+                load_issue(x);  // task t + PF, in flight under what follows
                 u8 *xb = xbuf[t & 1] + e * E * SP + 16 * lane;
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
@@ -415,7 +426,7 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
                     }
                 }
             } else {
-                load_task(x);
+                load_issue(x);
             }
             __syncthreads();
         };
@@ -547,10 +558,12 @@ int launch_wsp(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *di
 
 template <int E, int HW, int PF>
 int launch_wsp_mode(int k, hipStream_t st, const nkfs_geom &g, const u8 *ids, u64 *dig, u32 ngroups, u32 grid,
-                    bool nt)
+                    bool nt, bool dyn)
 {
     if (g.block_sizes)
         return launch_wsp<E, HW, PF, true, true>(k, st, g, ids, dig, ngroups, grid, nt);
+    if (dyn)
+        return launch_wsp<E, HW, PF, false, true>(k, st, g, ids, dig, ngroups, grid, nt);
     return launch_wsp<E, HW, PF, false, false>(k, st, g, ids, dig, ngroups, grid, nt);
 }
 
@@ -574,15 +587,31 @@ extern "C" int nkfs_wsp_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t 
     const u64 ngroups = (u64(g->nstripes) + S - 1) / S;
     const u32 cus = u32(nkfs_cu_count());
     const u32 grid = u32(ngroups < cus ? ngroups : cus);
-    const u8 *id8 = ids;
+    // uniform batches: groups from a device-wide counter as well (a CU whose
+    // HBM share runs slower takes fewer groups; the static walk -- workgroup
+    // b: groups b, b + grid, ... -- measured 0.4 % slower on C3), the
+    // counter a zeroed word of the launch's scratch; static when every
+    // workgroup has one group
+    const bool dyn = !g->block_sizes && ngroups > grid;
+    nkfs_geom g2 = *g;
+    Scratch sc;
+    if (dyn && !g2.queue) {
+        g2.queue = static_cast<u32 *>(sc.take(g, 256, st));
+        if (!g2.queue || hipMemsetAsync(g2.queue, 0, 4, st) != hipSuccess) {
+            (void)hipGetLastError();
+            sc.finish();
+            return -ENOSYS;
+        }
+    }
     int rc;
     if (e4)
-        rc = t.enc_ws_prefetch >= 2 ? launch_wsp_mode<4, 1, 2>(g->k, st, *g, id8, digests, u32(ngroups), grid, nt)
-                                    : launch_wsp_mode<4, 1, 1>(g->k, st, *g, id8, digests, u32(ngroups), grid, nt);
+        rc = t.enc_ws_prefetch >= 2 ? launch_wsp_mode<4, 1, 2>(g2.k, st, g2, ids, digests, u32(ngroups), grid, nt, dyn)
+                                    : launch_wsp_mode<4, 1, 1>(g2.k, st, g2, ids, digests, u32(ngroups), grid, nt, dyn);
     else
-        rc = t.enc_ws_prefetch >= 2 ? launch_wsp_mode<8, 2, 2>(g->k, st, *g, id8, digests, u32(ngroups), grid, nt)
-                                    : launch_wsp_mode<8, 2, 1>(g->k, st, *g, id8, digests, u32(ngroups), grid, nt);
-    if (rc)
-        return rc;
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+        rc = t.enc_ws_prefetch >= 2 ? launch_wsp_mode<8, 2, 2>(g2.k, st, g2, ids, digests, u32(ngroups), grid, nt, dyn)
+                                    : launch_wsp_mode<8, 2, 1>(g2.k, st, g2, ids, digests, u32(ngroups), grid, nt, dyn);
+    if (!rc && hipGetLastError() != hipSuccess)
+        rc = -EIO;
+    const int e = sc.finish();
+    return rc ? rc : e;
 }

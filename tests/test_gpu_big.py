@@ -150,8 +150,10 @@ def test_big_decode_matches(L, O, n, k, B, S):
     if S > 2:
         ids2[2, :] = ids2[2, 0]
     outs = []
-    for kern in ("generic", "big", "auto"):
-        with _tuned(dec_kernel=_lib.DEC[kern]):
+    # the column-chunked decoder, then the replicated-table decoder
+    # (nk8_bign.hip) in its three table layouts
+    for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2)):
+        with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
             torch.cuda.synchronize()
@@ -198,4 +200,11 @@ def test_big_round_trip_w2(L, O):
     out, status = batch.decode(parts, n, ids, avail, k, B)
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
+    assert torch.equal(out, blocks[:, :B])
+    for mode in (0, 1, 2):  # the replicated-table decoder on the bench's batch
+        with _tuned(dec_bign=mode):
+            out2, status2 = batch.decode(parts, n, ids, avail, k, B)
+        torch.cuda.synchronize()
+        assert int(status2.abs().sum()) == 0 and torch.equal(out2, out), mode
+        del out2
     assert torch.equal(out, blocks[:, :B])

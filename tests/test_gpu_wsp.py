@@ -53,6 +53,9 @@ def _enc(name):
                                      (1031, 2048, 7, 7)])
 @pytest.mark.parametrize("pf", [1, 2])
 def test_wsp_uniform_matches(L, O, S, B, n, k, pf):
+    """Uniform batches (groups from the device-wide counter; static when
+    every workgroup has one group: S = 5) against the fused kernel and the
+    oracle."""
     from nkfs_amd import batch
     blocks = batch.synth(S, B, first=91)
     ids_np = synth.batch_ids(S, n, first=91)
@@ -131,9 +134,9 @@ def test_wsp_ragged_matches(L, O, n, k, gap, mix, pf):
 
 
 def test_wsp_default_dispatch_c5_scale(L, O):
-    """enc_persist = 1: the automatic choice takes the persistent encoder for
-    C5 (ragged) and C3/C4 shapes (uniform); the C5 layout at the bench's
-    scale (11,520 stripes, ~4 GiB) gives the walk encoder's bytes."""
+    """enc_persist = 1 (default): the automatic choice takes the persistent
+    encoder for C5 (ragged); at the bench's scale and layout (11,520 stripes,
+    ~4 GiB) it gives the walk encoder's (enc_persist = 0) bytes."""
     from nkfs_amd import batch
     n, k = 8, 5
     sizes = synth.mixed_sizes(11520, (4096, 65536, 1048576))
