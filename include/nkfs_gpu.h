@@ -103,9 +103,11 @@ struct nkfs_tune {
 	int enc_persist;      /* n > 4 with digests: the persistent warp-specialised encoder (NKFS_ENC_WSP) where the
 	                         automatic choice is the walk encoder (ragged batches: 1, the default) or also the
 	                         warp-specialised grid (uniform batches: 2); 0 = off */
-	int dec_bign;         /* k > 8 decode on the replicated-table decoder (nk8_bign.hip): -1 = off (survivor-table /
-	                         column-chunked decoders), 0 = byte tables, 1 = byte tables x 2 replicas, 2 = nibble
-	                         tables x 16 replicas (every lookup in its lane's own bank slot) */
+	int dec_bign;         /* k > 8 decode on the stage-free decoder (nk8_bign.hip): -2 = auto (byte tables for
+	                         k > 16 and k % 4 == 0 below 16), -1 = off (survivor-table / column-chunked
+	                         decoders), 0 = byte tables, 1 = nibble tables x 16 replicas (every
+	                         lookup in its lane's own bank slot) in 16-survivor chunks, 2 = the same in 8-survivor
+	                         chunks (two workgroups per CU) */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

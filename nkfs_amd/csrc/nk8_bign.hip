@@ -1,36 +1,39 @@
-// nk8_bign.hip -- decode for k > 8 with replicated product tables: every
-// lookup of a wave lands in its own LDS bank slot.
+// nk8_bign.hip -- decode for k > 8 without an LDS stage and with product
+// tables whose lookups stay in their lanes' own bank slots.
 //
 // Reference arithmetic: crt/nk8.c:552-582 -- block[j*k+m] = XOR_c part_c[j]
 // W[c][m], W the inverse of the first k distinct survivors' Vandermonde rows
 // (k_decode_prep leaves the selection and W in `work`).
 //
 // k_decode_big / k_decode_wide look up packed 16-byte products U_c[x] =
-// (W[c][m0] x, ..., W[c][m0+15] x) with one ds_read_b128 per (row, survivor).
-// The index x is a data byte, so the 16 lanes of a b128 lane group pick
-// their 16-byte slots of a bank row at random: 3.07 passes per group on
-// average instead of 1 (the expected fullest of 16 random bins), and the
-// kernels are bound by LDS cycles (profiles/r03/sq_w2_summary.txt: LDS
-// active 86 % with an 85 % conflict share).  Here the tables are laid out so
-// that lane l's entries always sit in bank slot l & 15 (MODE 2) or in one of
-// two slot sets by lane parity (MODE 1):
+// (W[c][m0] x, ..., W[c][m0+15] x) with one ds_read_b128 per (row, survivor)
+// from a survivor stage in LDS.  The index x is a data byte, so the 16 lanes
+// of a b128 lane group pick their 16-byte bank slots at random: 3.07 passes
+// per group on average instead of 1 (the expected fullest of 16 random
+// bins), and those kernels are bound by LDS cycles (profiles/r03/
+// sq_w2_summary.txt: LDS active 86 % with an 85 % conflict share).
 //
-//  MODE 2  nibble tables, 16 replicas: U_c[x] = L_c[x & 15] ^ H_c[x >> 4];
-//          L_c[v] at c*4096 + v*256 + slot, H_c[v] at 64 KiB + v*4096 +
-//          c*256 + slot (slot = 16*(lane & 15)).  Both addresses come from
-//          one v_perm (byte q of the survivors' dword next to the slot byte)
-//          and one AND / AND-OR; two conflict-free lookups (8 LDS cycles per
-//          wave for 16 products x 64 rows) instead of one random one (~12).
-//  MODE 1  byte tables, 2 replicas: U_c[x] at c*8192 + x*32 + 16*(lane & 1)
-//          (v_perm + shift); 8 lanes per slot set: 2.6 passes per group.
-//  MODE 0  byte tables, 1 copy (64 KiB), the same loop: the A/B baseline.
+// Here a lane owns 4 consecutive rows: one dword of each of a chunk's CW
+// survivor parts (coalesced buffer loads, 256 B per wave instruction) feeds
+// its 4 rows directly -- v_perm places the row's byte next to the lane's
+// slot byte, so the LDS address needs no shift or add.  Table layouts
+// (struct nkfs_tune.dec_bign):
 //
-// Workgroup = (stripe, group of 16 output columns, slice of 2,048*T rows), 8
-// waves; lane = 4 consecutive rows: one dword of each of a chunk's 16
-// survivor parts (coalesced, 256 B per wave instruction) feeds its 4 rows
-// directly (v_perm picks the row's byte), so no LDS stage is needed.  The
-// groups of a (stripe, slice) run back to back on one XCD (workgroup b on XCD
-// b mod 8), so the rows' output lines complete in its L2.
+//  0  byte tables: U_c[x] at c*4096 + x*16 (64 KiB, CW = 16): random slots.
+//  1  nibble tables, 16 replicas: U_c[x] = L_c[x & 15] ^ H_c[x >> 4], each
+//     entry stored once per bank slot, lane l reading slot l & 15: every
+//     lookup conflict-free (two per product instead of one random).
+//     L_c[v] at c*4096 + v*256 + slot, H_c[v] 64 KiB higher (CW = 16, 128
+//     KiB: one workgroup per CU).
+//  2  the same nibble tables for CW = 8 survivors per chunk (64 KiB): two
+//     workgroups per CU, H_c at 32 KiB.
+//
+// Workgroup = (stripe, group of 16 output columns, slice of ROWS rows);
+// chunks of CW survivors: table build, then every row quad of the slice.
+// The groups of a (stripe, slice) run back to back on one XCD (workgroup b
+// on XCD b mod 8), so the rows' output lines complete in its L2.  For k <=
+// 16 (one group) with k % 4 == 0 a row quad is 4k contiguous output bytes,
+// written with dword stores.
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
@@ -43,14 +46,28 @@ using namespace nkfs::dev;
 
 namespace {
 
-constexpr int BN_T = 4;                        // row quads per lane per slice
-constexpr int BN_WAVES = 8;
-constexpr u32 BN_ROWS = 64u * BN_WAVES * 4u * BN_T;   // rows per workgroup slice (8,192)
-
+// launch shape per table layout: survivors per chunk, table bytes, waves
+// per workgroup, row quads per lane per slice and workgroups per CU
 template <int MODE>
-struct BnLayout {
-    static constexpr u32 bytes = MODE == 0 ? 65536u : 131072u;
+struct BnShape {
+    static constexpr int CW = MODE == 2 ? 8 : 16;
+    static constexpr u32 TBYTES = MODE == 1 ? 131072u : 65536u;
+    static constexpr int WAVES = MODE == 1 ? 16 : 8;
+    static constexpr int T = 2;
+    static constexpr int PER_CU = MODE == 1 ? 1 : 2;
+    static constexpr u32 ROWS = 64u * WAVES * 4u * T;   // 8,192 / 4,096 rows per slice
+    static constexpr u32 HI = MODE == 2 ? 32768u : 0u;  // H_c offset by immediate (MODE 1: by the slot word)
 };
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a release
+// fence over all memory and waits for every load in flight (vmcnt(0)),
+// which would drain the survivor prefetch at every table build.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler
 // emits two v_xor_b32 for it
@@ -72,208 +89,306 @@ __device__ __forceinline__ u32 load4_any(const u8 *p, u32 left)
     return w;
 }
 
-template <int MODE, bool PAL>
-__global__ __launch_bounds__(64 * BN_WAVES, 1) void k_decode_bign(nkfs_geom g, const u8 *work, const int32_t *status,
-                                                                 u32 ngroups, u32 nslices)
+// ONE: k <= CW, a single chunk: the workgroup builds its tables once and
+// walks slices wi, wi + nwg, ... of its stripe (the next slice's first
+// survivor loads in flight under the current one's last quad); otherwise
+// one slice per workgroup (nwg = nslices), tables rebuilt per chunk.
+template <int MODE, bool PAL, bool ONE>
+__global__ __launch_bounds__(64 * BnShape<MODE>::WAVES, BnShape<MODE>::PER_CU) void k_decode_bign(
+    nkfs_geom g, const u8 *work, const int32_t *status, u32 ngroups, u32 nslices, u32 nwg)
 {
-    __shared__ __attribute__((aligned(16))) u8 tbl[BnLayout<MODE>::bytes];
+    using SH = BnShape<MODE>;
+    constexpr int CW = SH::CW, WAVES = SH::WAVES, T = SH::T, NT = 64 * WAVES;
+    constexpr bool NIB = MODE != 0;
+    __shared__ __attribute__((aligned(16))) u8 tbl[SH::TBYTES];
+    __shared__ __attribute__((aligned(16))) u32 wq[CW][4];  // a chunk's W rows, columns 16h ..
+    __shared__ u32 wslot[CW];                               // a chunk's survivor slots
+
     const u32 b = blockIdx.x;
     const u32 loc = b >> 3;
     const u32 h = loc % ngroups;
-    const u32 slice = (loc / ngroups) % nslices;
-    const u32 s = (loc / ngroups / nslices) * 8 + (b & 7);
+    const u32 wi = (loc / ngroups) % nwg;
+    const u32 s = (loc / ngroups / nwg) * 8 + (b & 7);
     if (s >= g.nstripes || (status && status[s]))
         return;  // the whole workgroup
     const Stripe v = stripe_at(g, s);  // g.blocks = the output, g.n = slots per stripe
-    const u32 r_begin = slice * BN_ROWS;
-    if (r_begin >= v.ps)
+    if (wi * SH::ROWS >= v.ps)
         return;
     const int k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const u8 *wk = work + u64(s) * u64(k + k * k);
 
-    // the slot byte of this lane's table entries
-    // (MODE 2: byte 2 = 1 puts the high-nibble tables' addresses at 64 KiB)
-    const u32 slotv = MODE == 2 ? 0x10000u | u32(lane & 15) * 16u : MODE == 1 ? u32(lane & 1) * 128u : 0u;
+    // the lane's slot byte (byte 0 of every table address); MODE 1 puts the
+    // H tables 64 KiB up through byte 2 of the high lookups' slot word
+    const u32 slot_lo = NIB ? u32(lane & 15) * 16u : 0u;
+    const u32 slot_hi = slot_lo | (MODE == 1 ? 0x10000u : 0u);
 
-    uint4 acc[BN_T][4];
+    uint4 acc[T][4];
+
+    // CW*16 + CW bytes per chunk: item i < CW*16 is byte (i & 15) of chunk
+    // row i >> 4 of W (columns 16h ..), the next CW the survivor slot
+    // numbers (0 past k); thread tid fetches items tid and tid + NT one
+    // chunk ahead, so a table build never waits for HBM.  The raw bytes and
+    // their liveness are kept apart, so the loads stay in flight until the
+    // next chunk's LDS write uses them.
+    constexpr int NW = CW * 16, NI = NW + CW;
+    auto wsrc = [&](int cc, int i, bool &live) -> const u8 * {
+        if (i >= NW) {
+            const int c = CW * cc + (i - NW);
+            live = i < NI && c < k;
+            return wk + (live ? c : 0);
+        }
+        const int c = CW * cc + (i >> 4), m = 16 * int(h) + (i & 15);
+        live = c < k && m < k;
+        return wk + k + (live ? c * k + m : 0);  // clamped: no branch
+    };
+    bool wl0, wl1 = false;
+    u8 wr0 = *wsrc(0, tid, wl0), wr1 = 0;
+    if (tid + NT < NI)
+        wr1 = *wsrc(0, tid + NT, wl1);
+    auto wput = [&](int i, u32 wv) {
+        if (i < NW)
+            reinterpret_cast<u8 *>(wq)[i] = u8(wv);
+        else if (i < NI)
+            wslot[i - NW] = wv;
+    };
+
+    // survivor loads through one buffer resource over the stripe's slots
+    // (PAL; the launcher checks n * pitch < 2^31): offset = slot * pitch +
+    // row, no branch; rows past a part read its neighbour (rows never
+    // stored) or 0 past the slots, survivors past k read slot 0's part into
+    // a zero table.  Without PAL (ragged batches, unaligned parts): byte
+    // loads, clamped.
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u8 *>(v.parts), (short)0, int(u64(g.n) * v.pitch), 0x00020000);
+
+    const int nch = ONE ? 1 : (k + CW - 1) / CW;
+    u32 d0[CW], d1[CW];
+    u32 soff[CW];
+    auto load = [&](u32 (&d)[CW], u32 rb, int t, int cc) {
+        const u32 r4 = rb + (u32(t) * u32(NT) + u32(tid)) * 4u;
 #pragma unroll
-    for (int t = 0; t < BN_T; ++t)
+        for (int j = 0; j < CW; ++j) {
+            if constexpr (PAL) {
+                d[j] = __builtin_amdgcn_raw_buffer_load_b32(prs, soff[j] + r4, 0, 0);
+            } else {
+                const bool ok = CW * cc + j < k && r4 < v.ps;
+                d[j] = ok ? load4_any(v.parts + soff[j] + r4, v.ps - r4) : 0u;
+            }
+        }
+    };
+    for (u32 slice = wi;; slice += nwg) {
+    const u32 r_begin = slice * SH::ROWS;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             acc[t][q] = make_uint4(0, 0, 0, 0);
-
-    const int nch = (k + 15) / 16;
+    const u32 next = slice + nwg;
+    const bool more = ONE && next * SH::ROWS < v.ps;
     for (int cc = 0; cc < nch; ++cc) {
-        __syncthreads();  // the previous chunk's lookups are done
-        // ---- tables of survivors 16cc .. 16cc+15 for output columns 16h ..
-        if constexpr (MODE == 2) {
-            // 32 (kind, column) pairs x 4 wave writes of 4 value rows x 16
-            // replicas; wave w takes pairs w, w + 8, w + 16, w + 24
+      if (!ONE || slice == wi) {
+        lds_barrier();  // the previous chunk's lookups are done
+        wput(tid, wl0 ? u32(wr0) : 0u);
+        if (tid + NT < NI)
+            wput(tid + NT, wl1 ? u32(wr1) : 0u);
+        if (cc + 1 < nch) {
+            wr0 = *wsrc(cc + 1, tid, wl0);
+            if (tid + NT < NI)
+                wr1 = *wsrc(cc + 1, tid + NT, wl1);
+        }
+        lds_barrier();
+
+#pragma unroll
+        for (int j = 0; j < CW; ++j)
+            soff[j] = CW * cc + j < k ? u32(u64(wslot[j]) * v.pitch) : 0u;
+        // the first quad's survivor loads fly while the tables are built
+        load(d0, r_begin, 0, cc);
+
+        // ---- tables of the chunk's survivors for output columns 16h ..
+        if constexpr (NIB) {
+            // (kind, column) pairs x 4 wave writes of 4 value rows x 16
+            // replicas: lane l writes value 4 it + l / 16 into slot l & 15
 #pragma unroll 1
-            for (int pi = wave; pi < 32; pi += BN_WAVES) {
-                const int kind = pi >> 4, j = pi & 15, c = 16 * cc + j;
-                u32 row[4] = {0, 0, 0, 0};
-                if (c < k)
-                    for (int e = 0; e < 16; ++e) {
-                        const int m = 16 * int(h) + e;
-                        if (m < k)
-                            row[e >> 2] |= u32(wk[k + c * k + m]) << (8 * (e & 3));
+            for (int pi = wave; pi < 2 * CW; pi += WAVES) {
+                const int kind = pi / CW, j = pi % CW;  // wave-uniform
+                // basis of the kind's nibble: row * 2^(4 kind + b), b < 4
+                u32 bs[4][4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    u32 x = wq[j][w];
+                    if (kind)
+                        x = gf_xtime4(gf_xtime4(gf_xtime4(gf_xtime4(x))));
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb) {
+                        bs[bb][w] = x;
+                        x = gf_xtime4(x);
                     }
-                u32 basis[8][4];
-                make_basis<4>(basis, row);
+                }
+                const u32 base = u32(j) * 4096u + (kind ? (MODE == 1 ? 65536u : SH::HI) : 0u);
 #pragma unroll
                 for (int it = 0; it < 4; ++it) {
-                    const int vv = 4 * it + (lane >> 4);
+                    const u32 vv = u32(4 * it) + u32(lane >> 4);
                     u32 e4[4] = {0, 0, 0, 0};
 #pragma unroll
-                    for (int bb = 0; bb < 4; ++bb)
-                        if ((vv >> bb) & 1)
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const u32 msk = 0u - ((vv >> bb) & 1u);  // branch-free select of the bit's basis
 #pragma unroll
-                            for (int w = 0; w < 4; ++w)
-                                e4[w] ^= basis[4 * kind + bb][w];
-                    const u32 addr = kind == 0 ? u32(j) * 4096u + u32(vv) * 256u + u32(lane & 15) * 16u
-                                               : 65536u + u32(vv) * 4096u + u32(j) * 256u + u32(lane & 15) * 16u;
-                    *reinterpret_cast<uint4 *>(tbl + addr) = make_uint4(e4[0], e4[1], e4[2], e4[3]);
+                        for (int w = 0; w < 4; ++w)
+                            e4[w] ^= bs[bb][w] & msk;
+                    }
+                    *reinterpret_cast<uint4 *>(tbl + base + vv * 256u + u32(lane & 15) * 16u) =
+                        make_uint4(e4[0], e4[1], e4[2], e4[3]);
                 }
             }
         } else {
-            // byte tables: column j, entries x = 32 m + (lane >> (MODE)) ...;
-            // MODE 1: replica lane & 1, 32 entries per wave write; MODE 0:
-            // 64 entries per wave write
-            constexpr int EPW = MODE == 1 ? 32 : 64;  // entries per wave write
-            constexpr int NW = 256 / EPW;             // wave writes per column
+            // byte tables: column j, entries x = lane + 64 m (Gray-code walk
+            // over the two high bits, one XOR per entry)
 #pragma unroll 1
-            for (int j = wave; j < 16; j += BN_WAVES) {
-                const int c = 16 * cc + j;
-                u32 row[4] = {0, 0, 0, 0};
-                if (c < k)
-                    for (int e = 0; e < 16; ++e) {
-                        const int m = 16 * int(h) + e;
-                        if (m < k)
-                            row[e >> 2] |= u32(wk[k + c * k + m]) << (8 * (e & 3));
-                    }
+            for (int j = wave; j < CW; j += WAVES) {
+                const u32 row[4] = {wq[j][0], wq[j][1], wq[j][2], wq[j][3]};
                 u32 basis[8][4];
                 make_basis<4>(basis, row);
-                const int x0 = MODE == 1 ? (lane >> 1) : lane;
-                constexpr int LB = MODE == 1 ? 5 : 6;  // low bits fixed per lane
                 u32 hv[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int bb = 0; bb < LB; ++bb)
-                    if ((x0 >> bb) & 1)
+                for (int bb = 0; bb < 6; ++bb) {
+                    const u32 msk = 0u - ((u32(lane) >> bb) & 1u);
 #pragma unroll
-                        for (int w = 0; w < 4; ++w)
-                            hv[w] ^= basis[bb][w];
+                    for (int w = 0; w < 4; ++w)
+                        hv[w] ^= basis[bb][w] & msk;
+                }
 #pragma unroll
-                for (int mi = 0; mi < NW; ++mi) {
+                for (int mi = 0; mi < 4; ++mi) {
                     if (mi) {
                         const int bit = __builtin_ctz(mi);
 #pragma unroll
                         for (int w = 0; w < 4; ++w)
-                            hv[w] ^= basis[LB + bit][w];
+                            hv[w] ^= basis[6 + bit][w];
                     }
-                    const int x = x0 + EPW * (mi ^ (mi >> 1));
-                    const u32 addr = MODE == 1 ? u32(j) * 8192u + u32(x) * 32u + u32(lane & 1) * 16u
-                                               : u32(j) * 4096u + u32(x) * 16u;
-                    *reinterpret_cast<uint4 *>(tbl + addr) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+                    const int x = lane + 64 * (mi ^ (mi >> 1));
+                    *reinterpret_cast<uint4 *>(tbl + u32(j) * 4096u + u32(x) * 16u) =
+                        make_uint4(hv[0], hv[1], hv[2], hv[3]);
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
+      }
 
-        // ---- survivor part bases of the chunk (zero table past k)
-        const u8 *src[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int c = 16 * cc + j;
-            src[j] = v.parts + (c < k ? u64(wk[c]) * v.pitch : 0);
-        }
-        auto load = [&](u32 (&d)[16], int t) {
-            const u32 r4 = r_begin + (u32(t) * 64u * BN_WAVES + u32(tid)) * 4u;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const bool ok = 16 * cc + j < k && r4 < v.ps;
-                if constexpr (PAL)
-                    d[j] = ok ? *reinterpret_cast<const u32 *>(src[j] + r4) : 0u;
-                else
-                    d[j] = ok ? load4_any(src[j] + r4, v.ps - r4) : 0u;
-            }
-        };
-        // quad t's dwords in dc, quad t+1's loads in flight in dn; the
-        // quads' accumulators rotate by one per quad (back in order after
-        // BN_T), so the loop is not unrolled and every index stays static
-        u32 dc[16], dn[16];
-        load(dc, 0);
-#pragma unroll 1
-        for (int t = 0; t < BN_T; ++t) {
-            if (t + 1 < BN_T)
-                load(dn, t + 1);
-            // tdep (0 at run time) chains each survivor's lookups behind the
-            // previous survivor's XORs: unchained, the compiler hoists all
-            // 64 (128) lookups of a quad and spills
+        // one row quad: the CW survivors' products into a4[q] (row 4i + q);
+        // tdep (0 at run time) links groups of 16 lookups, so the compiler
+        // keeps 16 in flight instead of hoisting all of them (spills)
+        auto quad = [&](const u32 (&d)[CW], uint4 (&a4)[4], int cc) {
             u32 tdep = 0;
-            uint4 a4[4] = {acc[0][0], acc[0][1], acc[0][2], acc[0][3]};
-            if constexpr (MODE == 2) {
+            if constexpr (NIB) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const u32 sv = slotv + tdep;
+                for (int j = 0; j < CW; ++j) {
+                    if (CW * cc + j >= k)
+                        break;  // survivors past k (uniform): their tables are zero
+                    const u32 dl = d[j] & 0x0F0F0F0Fu, dh = (d[j] >> 4) & 0x0F0F0F0Fu;
+                    const u32 sl = slot_lo + tdep, sh = slot_hi + tdep;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        // P = 1 << 16 | (byte q of the survivor dword) << 8 | slot
-                        const u32 P = __builtin_amdgcn_perm(dc[j], sv, 0x0C020000u | (u32(4 + q) << 8));
-                        const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + (P & 0x0FFFu));
-                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 256u + (P & 0x1F0FFu));
+                        // (nibble of row q's byte) << 8 | slot byte (| 1 << 16)
+                        const u32 sel = 0x0C020000u | (u32(4 + q) << 8);
+                        const u32 Pl = __builtin_amdgcn_perm(dl, sl, sel), Ph = __builtin_amdgcn_perm(dh, sh, sel);
+                        const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + Pl);
+                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + SH::HI + Ph);
                         a4[q].x = xor3(a4[q].x, a.x, c2.x);
                         a4[q].y = xor3(a4[q].y, a.y, c2.y);
                         a4[q].z = xor3(a4[q].z, a.z, c2.z);
                         a4[q].w = xor3(a4[q].w, a.w, c2.w);
                     }
-                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
+                    if (j & 1)
+                        asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
                 }
             } else {
-                // survivors in pairs: one three-input XOR per word folds both lookups
+                // survivors in pairs: one three-input XOR per word folds both
 #pragma unroll
-                for (int j = 0; j < 16; j += 2) {
-                    const u32 sv = slotv + tdep;
+                for (int j = 0; j < CW; j += 2) {
+                    if (CW * cc + j >= k)
+                        break;  // survivors past k (uniform): their tables are zero
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const u32 sel = 0x0C0C0000u | (u32(4 + q) << 8);
-                        const u32 P0 = __builtin_amdgcn_perm(dc[j], sv, sel), P1 = __builtin_amdgcn_perm(dc[j + 1], sv, sel);
-                        constexpr u32 CS = MODE == 1 ? 8192u : 4096u;  // column stride
-                        constexpr int SH = MODE == 1 ? 3 : 4;          // x << 8 -> x * 32 (+ replica) / x * 16
-                        const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * CS + (P0 >> SH));
-                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * CS + (P1 >> SH));
+                        // (row q's byte) << 4: the 16-byte entry of the table
+                        const u32 sel = 0x0C0C0C00u | u32(4 + q);
+                        const u32 P0 = (__builtin_amdgcn_perm(d[j], 0u, sel) << 4) + tdep;
+                        const u32 P1 = (__builtin_amdgcn_perm(d[j + 1], 0u, sel) << 4) + tdep;
+                        const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
+                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
                         a4[q].x = xor3(a4[q].x, a.x, c2.x);
                         a4[q].y = xor3(a4[q].y, a.y, c2.y);
                         a4[q].z = xor3(a4[q].z, a.z, c2.z);
                         a4[q].w = xor3(a4[q].w, a.w, c2.w);
                     }
-                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
+                    if (j & 2)
+                        asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
                 }
             }
-#pragma unroll
-            for (int i = 0; i + 1 < BN_T; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[i][q] = acc[i + 1][q];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                acc[BN_T - 1][q] = a4[q];
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                dc[j] = dn[j];
-        }
+        };
+        // two named buffers of survivor dwords (quad 0 in one, quad 1's
+        // loads in flight in the other: the compiler's wait covers only the
+        // loads a quad consumes)
+        static_assert(T == 2, "one pass of two quads per chunk");
+        load(d1, r_begin, 1, cc);
+        quad(d0, acc[0], cc);
+        if constexpr (ONE)  // the next slice's first quad (its rows, or these again past the end)
+            load(d0, more ? next * SH::ROWS : r_begin, 0, cc);
+        quad(d1, acc[1], cc);
     }
 
-    // row r's bytes 16h..16h+15 at r*k + 16h (fewer in the last group;
-    // nothing at or past B)
+    // ---- output: row r's columns 16h .. at r*k + 16h (nothing at or past B)
     u8 *out = const_cast<u8 *>(v.blk);
     const uintptr_t oa = reinterpret_cast<uintptr_t>(out);
+    if (ngroups == 1 && (oa & 15) == 0 && (u32(k) & 3) == 0) {
+        // k in {4, 8, 12, 16}, 16-aligned block: the quad's 4 rows are 4k
+        // contiguous bytes = the first k/4 dwords of each row's accumulator;
+        // written as k/4 16-byte stores (a wave's fill 256k contiguous bytes)
+        const u32 kd = u32(k) >> 2;
 #pragma unroll
-    for (int t = 0; t < BN_T; ++t) {
+        for (int t = 0; t < T; ++t) {
+            const u32 r0 = r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u;
+            if (r0 >= v.ps)
+                continue;
+            const u64 base = u64(r0) * u64(k);
+            const uint4 a0 = acc[t][0], a1 = acc[t][1], a2 = acc[t][2], a3 = acc[t][3];
+            u8 *o = out + base;
+            if (base + 4u * u64(k) <= u64(v.B)) {
+                switch (kd) {  // row q's dwords are its accumulator's first kd
+                case 1:
+                    store16(o, a0.x, a1.x, a2.x, a3.x, false);
+                    break;
+                case 2:
+                    store16(o, a0.x, a0.y, a1.x, a1.y, false);
+                    store16(o + 16, a2.x, a2.y, a3.x, a3.y, false);
+                    break;
+                case 3:
+                    store16(o, a0.x, a0.y, a0.z, a1.x, false);
+                    store16(o + 16, a1.y, a1.z, a2.x, a2.y, false);
+                    store16(o + 32, a2.z, a3.x, a3.y, a3.z, false);
+                    break;
+                default:
+                    store16(o, a0.x, a0.y, a0.z, a0.w, false);
+                    store16(o + 16, a1.x, a1.y, a1.z, a1.w, false);
+                    store16(o + 32, a2.x, a2.y, a2.z, a2.w, false);
+                    store16(o + 48, a3.x, a3.y, a3.z, a3.w, false);
+                }
+            } else {  // the block's last rows
+                const uint4 aq[4] = {a0, a1, a2, a3};
+                for (u32 c = 0; c < 4u * u32(k); ++c) {
+                    const u32 q = c / u32(k), e = c % u32(k);
+                    const uint4 x = aq[q];
+                    const u32 wd = e < 4 ? x.x : e < 8 ? x.y : e < 12 ? x.z : x.w;
+                    if (base + c < u64(v.B))
+                        o[c] = u8(wd >> (8 * (e & 3)));
+                }
+            }
+        }
+    } else {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const u32 r = r_begin + (u32(t) * 64u * BN_WAVES + u32(tid)) * 4u + u32(q);
+            const u32 r = r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u + u32(q);
             if (r >= v.ps)
                 continue;
             const u64 rb = u64(r) * u64(k);
@@ -294,18 +409,41 @@ __global__ __launch_bounds__(64 * BN_WAVES, 1) void k_decode_bign(nkfs_geom g, c
             }
         }
     }
+    }
+    if (!more)
+        break;
+    }
 }
 
 template <int MODE>
-int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, u32 ngroups, u32 nslices, u64 grid,
-                bool pal, hipStream_t st)
+int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, bool pal, hipStream_t st)
 {
-    if (pal)
-        hipLaunchKernelGGL((k_decode_bign<MODE, true>), dim3(u32(grid)), dim3(64 * BN_WAVES), 0, st, *g, work, status,
-                           ngroups, nslices);
+    const int k = g->k;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 ngroups = (u64(k) + 15) / 16;
+    const u64 nslices = (u64(ps_max) + BnShape<MODE>::ROWS - 1) / BnShape<MODE>::ROWS;
+    const u32 ns = u32(nslices ? nslices : 1);
+    // one chunk: workgroups per stripe enough for ~8 per CU in all, each
+    // walking its share of the slices with the tables built once
+    const bool one = k <= BnShape<MODE>::CW;
+    u32 nwg = ns;
+    if (one) {
+        const u64 want = (u64(nkfs_cu_count()) * 8 + u64(g->nstripes) - 1) / u64(g->nstripes);
+        nwg = u32(want < ns ? (want ? want : 1) : ns);
+    }
+    const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * nwg;
+    if (grid > 0x7FFFFFFFull)
+        return -EINVAL;
+    const dim3 block(64 * BnShape<MODE>::WAVES);
+    const u32 ng = u32(ngroups);
+    if (one && pal)
+        hipLaunchKernelGGL((k_decode_bign<MODE, true, true>), dim3(u32(grid)), block, 0, st, *g, work, status, ng, ns, nwg);
+    else if (one)
+        hipLaunchKernelGGL((k_decode_bign<MODE, false, true>), dim3(u32(grid)), block, 0, st, *g, work, status, ng, ns, nwg);
+    else if (pal)
+        hipLaunchKernelGGL((k_decode_bign<MODE, true, false>), dim3(u32(grid)), block, 0, st, *g, work, status, ng, ns, nwg);
     else
-        hipLaunchKernelGGL((k_decode_bign<MODE, false>), dim3(u32(grid)), dim3(64 * BN_WAVES), 0, st, *g, work,
-                           status, ngroups, nslices);
+        hipLaunchKernelGGL((k_decode_bign<MODE, false, false>), dim3(u32(grid)), block, 0, st, *g, work, status, ng, ns, nwg);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -313,7 +451,8 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 
 // Decode a uniform or ragged batch with 2 <= k <= 254 from the plan
 // k_decode_prep left in `work` (stripes with status != 0 are skipped), with
-// table layout `mode` (0 byte, 1 byte x 2 replicas, 2 nibble x 16 replicas).
+// table layout `mode` (0 byte tables, 1 nibble x 16 replicas in 16-survivor
+// chunks, 2 nibble x 16 replicas in 8-survivor chunks).
 extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int mode,
                                 hipStream_t st)
 {
@@ -324,18 +463,13 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
         return 0;
     if (u64(g->block_size) + 64u > 0x7FFFFFFFull)
         return -ENOSYS;
-    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
-    const u64 ngroups = (u64(k) + 15) / 16;
-    const u64 nslices = (u64(ps_max) + BN_ROWS - 1) / BN_ROWS;
-    const u64 grid = (u64(g->nstripes) + 7) / 8 * 8 * ngroups * (nslices ? nslices : 1);
-    if (grid > 0x7FFFFFFFull)
-        return -EINVAL;
-    // dword survivor loads: uniform batches with 4-byte aligned parts and pitch
-    const bool pal = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->parts) | g->part_pitch) & 3) == 0;
-    const u32 ng = u32(ngroups), ns = u32(nslices ? nslices : 1);
+    // dword survivor loads through a buffer resource over a stripe's slots:
+    // uniform batches with 4-byte aligned parts and pitch, slots < 2 GiB
+    const bool pal = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->parts) | g->part_pitch) & 3) == 0 &&
+                     u64(g->n) * g->part_pitch < 0x7FFFFFFFull;
     switch (mode) {
-    case 0: return launch_bign<0>(g, work, status, ng, ns, grid, pal, st);
-    case 1: return launch_bign<1>(g, work, status, ng, ns, grid, pal, st);
-    default: return launch_bign<2>(g, work, status, ng, ns, grid, pal, st);
+    case 0: return launch_bign<0>(g, work, status, pal, st);
+    case 1: return launch_bign<1>(g, work, status, pal, st);
+    default: return launch_bign<2>(g, work, status, pal, st);
     }
 }

@@ -911,11 +911,18 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         return rc;
     // k <= 16: survivor tables of 16-byte products (nk8_wide.hip); beyond:
     // 16-column chunks (nk8_big.hip); pinned GENERIC: thread per row
-    // dec_bign >= 0: the replicated-table decoder for every k > 8 (unless a
-    // family is pinned)
+    // the stage-free decoder (nk8_bign.hip): dec_bign >= 0 pins a table
+    // layout for every k > 8; -2 (auto, the default) takes byte tables where
+    // they win: k > 16 (W2 N48K32 1,315 -> 2,082 GB/s, N24K20 926 -> 1,211)
+    // and k % 4 == 0 below 16 (W1 N16K12 3,330 -> 4,296); k = 16 (4,087 /
+    // 3,952) and other k keep the survivor-table decoder
+    // (profiles/r05/ab_bign.txt)
     rc = -ENOSYS;
-    if (t.dec_bign >= 0 && (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG))
-        rc = nkfs_bign_decode(g, (const u8 *)work, status, t.dec_bign, st);
+    if (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG) {
+        const bool auto_pick = t.dec_bign == -2 && (g->k > 16 || (g->k % 4 == 0 && g->k < 16));
+        if (t.dec_bign >= 0 || auto_pick)
+            rc = nkfs_bign_decode(g, (const u8 *)work, status, t.dec_bign >= 0 ? t.dec_bign : 0, st);
+    }
     if (rc == -ENOSYS)
         rc = t.dec_kernel == NKFS_DEC_GENERIC || t.dec_kernel == NKFS_DEC_BIG
                  ? -ENOSYS

@@ -152,7 +152,8 @@ def test_big_decode_matches(L, O, n, k, B, S):
     outs = []
     # the column-chunked decoder, then the replicated-table decoder
     # (nk8_bign.hip) in its three table layouts
-    for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2)):
+    for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2),
+                       ("auto", -2)):
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
@@ -201,7 +202,7 @@ def test_big_round_trip_w2(L, O):
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     assert torch.equal(out, blocks[:, :B])
-    for mode in (0, 1, 2):  # the replicated-table decoder on the bench's batch
+    for mode in (-1, 0, 1, 2):  # the survivor-table decoder, the stage-free one's layouts
         with _tuned(dec_bign=mode):
             out2, status2 = batch.decode(parts, n, ids, avail, k, B)
         torch.cuda.synchronize()
