@@ -123,6 +123,11 @@ int nkfs_walk_offsets_fit(uint64_t block_size, uint64_t part_span, uint64_t nstr
 int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *block_size, uint32_t max_block_size,
 			uint32_t nstripes, int n_slots, int k, int navail, const uint64_t *part_off, uint32_t page_size,
 			uint64_t chunk_bytes, char *msg, size_t msg_len);
+/* The device of every host lane a host-memory call runs (CPU only, no GPU
+ * call): struct nkfs_tune.host_lanes lanes per device, interleaved over the
+ * devices (d0, d1, ..., d0, d1, ...) so a cap of max_lanes drops whole
+ * rounds, never a device.  Returns the number of lanes written. */
+int nkfs_host_lane_plan(const int *devices, int ndev, int per_device, int *lanes, int max_lanes);
 
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */
 uint32_t nkfs_part_size(uint32_t block_size, int k);

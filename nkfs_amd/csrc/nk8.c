@@ -40,13 +40,20 @@ static int rand_bytes(void *buf, size_t len)
 /* getrandom bytes drawn 256 at a time per thread: a drop-in split draws n
  * ids, one 8-byte word each (more on rejection), and a syscall per word
  * cost microseconds of a ~15 us call.  The words are the same uniform bytes
- * (crt/random.c draws from getrandom as well); a forked child continues its
- * parent's pool, which is harmless: ids only need to differ within a block. */
+ * (crt/random.c draws from getrandom as well).  The pool is tagged with the
+ * pid that filled it: a forked child refills instead of handing out its
+ * parent's next words (the reference draws fresh bytes per call). */
 static __thread uint8_t g_rpool[256];
 static __thread unsigned g_rpos = sizeof(g_rpool);
+static __thread pid_t g_rpid;
 
 static int rand_word(uint64_t *out)
 {
+	const pid_t me = getpid();
+	if (g_rpid != me) {
+		g_rpid = me;
+		g_rpos = sizeof(g_rpool);
+	}
 	if (g_rpos + sizeof(*out) > sizeof(g_rpool)) {
 		int err = rand_bytes(g_rpool, sizeof(g_rpool));
 		if (err)

@@ -85,6 +85,9 @@ struct BigChain {
     u64 *digests;   // [stripe][n]
 };
 
+// this wave's XCC (hardware register XCC_ID, bits 3:0)
+__device__ inline u32 xcc_id() { return u32(__builtin_amdgcn_s_getreg(20 | (3 << 11))) & 15u; }
+
 constexpr u64 CHAIN_TIMEOUT = 200000;  // s_memrealtime ticks (100 MHz): 2 ms (a slice takes ~35 us)
 
 template <bool HASH>
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             u32 f;
             for (;;) {
                 f = __builtin_amdgcn_raw_buffer_load_b32(fr, 0, 0, 1);
-                if (f >= slice || __builtin_amdgcn_raw_buffer_load_b32(xr, 0, 0, 1))
+                if ((f & 0xFFFFFFu) >= slice || __builtin_amdgcn_raw_buffer_load_b32(xr, 0, 0, 1))
                     break;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_TIMEOUT) {
                     if (lane == 0)
@@ -274,7 +277,13 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            hok = f >= slice && f != 0xFFFFFFFFu;
+            // the hand-off is only coherent inside one XCD's L2: the flag
+            // carries the producer's XCC id, and a chain whose
+            // producer ran elsewhere is treated as lost -- recomputed by
+            // k_big_hash_fix -- instead of trusting possibly stale lines
+            hok = f != 0xFFFFFFFFu && (f & 0xFFFFFFu) >= slice && (f >> 24) == xcc_id();
+            if (!hok && f != 0xFFFFFFFFu && (f & 0xFFFFFFu) >= slice && lane == 0)
+                __hip_atomic_store(ch.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (hok) {
                 const v2u w = __builtin_amdgcn_raw_buffer_load_b64(brsrc(ch.acc + u64(unit) * 64, 512),
                                                                    u32(16 * wave + (lane & 15)) * 8u, 0, 1);
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             __builtin_amdgcn_s_waitcnt(0);  // the accumulators are in the L2 before the flag
             __syncthreads();
             if (tid == 0)
-                __hip_atomic_store(ch.flag + unit, chain_bad ? 0xFFFFFFFFu : slice + 1, __ATOMIC_RELEASE,
+                __hip_atomic_store(ch.flag + unit, chain_bad ? 0xFFFFFFFFu : (xcc_id() << 24) | (slice + 1), __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
             const int base = lane & ~3;

@@ -886,6 +886,24 @@ static void *lane_main(void *arg)
 	return NULL;
 }
 
+int nkfs_host_lane_plan(const int *devices, int ndev, int per_device, int *lanes, int max_lanes)
+{
+	if (!devices || !lanes || ndev < 1 || max_lanes < 1)
+		return 0;
+	if (per_device < 1)
+		per_device = 1;
+	/* device-interleaved rounds (filling device by device let
+	 * the NKFS_MAX_DEVICES cap drop the trailing devices entirely) */
+	int nl = 0;
+	for (int j = 0; j < per_device; j++)
+		for (int i = 0; i < ndev; i++) {
+			if (nl == max_lanes)
+				return nl;
+			lanes[nl++] = devices[i];
+		}
+	return nl;
+}
+
 /* Pin the contiguous caller buffers, cut the batch over the device lanes
  * (byte-balanced contiguous stripe ranges) and run them. */
 static int hp_run(struct hp *h)
@@ -907,20 +925,12 @@ static int hp_run(struct hp *h)
 	int rc = pin_take2(rp, rb, held);
 	if (rc)
 		return rc;
-	int lanes[NKFS_MAX_DEVICES];
-	int nl = nkfs_gpu_get_devices(lanes, NKFS_MAX_DEVICES);
 	/* struct nkfs_tune.host_lanes host threads per device: each lane keeps
 	 * its own host_depth sub-batches in flight, so one host thread blocked
 	 * on a stream never leaves the link idle */
-	const int per = nkfs_host_lanes();
-	if (per > 1) {
-		int dv[NKFS_MAX_DEVICES], nd = nl;
-		memcpy(dv, lanes, sizeof(dv));
-		nl = 0;
-		for (int i = 0; i < nd; i++)
-			for (int j = 0; j < per && nl < NKFS_MAX_DEVICES; j++)
-				lanes[nl++] = dv[i];
-	}
+	int dv[NKFS_MAX_DEVICES], lanes[NKFS_MAX_DEVICES];
+	const int nd = nkfs_gpu_get_devices(dv, NKFS_MAX_DEVICES);
+	int nl = nkfs_host_lane_plan(dv, nd, nkfs_host_lanes(), lanes, NKFS_MAX_DEVICES);
 	if (nl > (int)h->nstripes)
 		nl = (int)h->nstripes;
 	if (nl <= 1) {

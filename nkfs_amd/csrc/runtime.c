@@ -455,6 +455,9 @@ int nkfs_ctx_events(struct nkfs_ctx *c)
  * costs ~4 us on a 4 KiB call, where the stream sync still spins, but the
  * sync's later wake-up costs 2-28 us from 64 KiB blocks on
  * (profiles/r04/percall_spin_vs_sync.txt), so callers spin from 32 KiB. */
+/* pause iterations a completion wait spins before it blocks (~1-2 ms) */
+#define NKFS_SPIN_MAX (16ull << 16)
+
 int nkfs_ctx_wait(struct nkfs_ctx *c, int spin)
 {
 #ifdef NKFS_WAIT_SYNC /* A/B builds: the plain stream sync */
@@ -481,13 +484,22 @@ int nkfs_ctx_wait(struct nkfs_ctx *c, int spin)
 		HIPCHK(hipStreamSynchronize(c->stream));
 		return 0;
 	}
-	for (uint64_t spin = 0; __atomic_load_n(c->done, __ATOMIC_ACQUIRE) != want; spin++) {
-		if ((spin & 0xFFFF) == 0xFFFF) {
+	/* spin on the completion word for a bounded time (a small call's late
+	 * stream-sync wake-up costs more than the call), then block in the
+	 * stream sync instead of burning a core for a long one */
+	for (uint64_t it = 0; __atomic_load_n(c->done, __ATOMIC_ACQUIRE) != want; it++) {
+		if ((it & 0xFFFF) == 0xFFFF) {
 			hipError_t q = hipStreamQuery(c->stream);
 			if (q != hipSuccess && q != hipErrorNotReady)
 				return nkfs_hip_fail("hipStreamQuery", (int)q);
 			if (q == hipSuccess && __atomic_load_n(c->done, __ATOMIC_ACQUIRE) != want)
 				return -EIO; /* the stream drained without the word */
+			if (it >= NKFS_SPIN_MAX) {
+				HIPCHK(hipStreamSynchronize(c->stream));
+				if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) != want)
+					return -EIO;
+				break;
+			}
 		}
 		__builtin_ia32_pause();
 	}

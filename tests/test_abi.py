@@ -228,3 +228,26 @@ def test_debug_bounds_build_compiles():
                              capture_output=True, text=True, check=True).stdout
     obj = subprocess.run(["grep", "-c", "nkfs bounds"], input=strings, capture_output=True, text=True)
     assert int(obj.stdout.strip() or 0) >= 1
+
+
+def test_host_lane_plan_interleaves_devices():
+    """the host lanes of a host-memory call go round-robin over
+    the devices, so the lane cap (16) drops whole rounds, never a device:
+    8 devices x 3 lanes -> every device gets 2 lanes; 9+ devices at 2 lanes
+    each keep every device."""
+    L = _lib.lib()
+
+    def plan(devs, per, cap=16):
+        d = (C.c_int * len(devs))(*devs)
+        out = (C.c_int * cap)()
+        n = L.nkfs_host_lane_plan(d, len(devs), per, out, cap)
+        return list(out[:n])
+
+    assert plan([0], 2) == [0, 0]
+    assert plan([0, 1], 1) == [0, 1]
+    p = plan(list(range(8)), 3)
+    assert len(p) == 16 and all(p.count(d) == 2 for d in range(8))
+    p = plan(list(range(10)), 2)
+    assert len(p) == 16 and set(p) == set(range(10))
+    assert plan(list(range(4)), 4) == [0, 1, 2, 3] * 4
+    assert plan([], 2) == [] and plan([3], 0) == [3]
