@@ -108,6 +108,10 @@ struct nkfs_tune {
 	                         decoders), 0 = byte tables, 1 = nibble tables x 16 replicas (every
 	                         lookup in its lane's own bank slot) in 16-survivor chunks, 2 = the same in 8-survivor
 	                         chunks (two workgroups per CU) */
+	int enc_bign;         /* k <= 32 encode on the stage-free encoder with a hash wave (nk8_bign.hip): -1 = auto
+	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64
+	                         pass), 1 = every k <= 32 batch it accepts, persistent (a workgroup per CU walking
+	                         the (stripe, part group) units), 2 = the same, one workgroup per unit */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

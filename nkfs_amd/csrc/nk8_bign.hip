@@ -38,13 +38,19 @@
 #include <errno.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "nk8_dev.h"
 #include "nkfs_internal.h"
+#include "runtime.h"
+#include "xxh64_dev.h"
 
 using namespace nkfs;
 using namespace nkfs::dev;
 
 namespace {
+
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 // launch shape per table layout: survivors per chunk, table bytes, waves
 // per workgroup, row quads per lane per slice and workgroups per CU
@@ -447,6 +453,359 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// ---- encode, k <= 32 ------------------------------------------------------
+// Reference arithmetic: crt/nk8.c:403-420 -- part_i[j] = XOR_m x_i^m
+// d[j*k+m], d zero past block_size (:393-398); XXH64 of every part
+// (crt/csum.c, crt/xxhash.c:791-916).
+//
+// Persistent: one workgroup of 16 waves per CU walks units = (stripe, group
+// of 16 parts).  Per unit the k <= 32 columns' byte tables U_m[x] =
+// (x_{p0}^m x, ..., x_{p0+15}^m x) are built once and stay resident (128
+// KiB).  Waves 0..14 encode: a lane owns 4 consecutive rows per slice of
+// 3,840 rows, loads each row's column bytes straight from the block
+// (dword-aligned 16 + 4-byte buffer loads and v_alignbyte -- no LDS stage),
+// looks up one 16-part product per (row, column), transposes its 4 rows x 16
+// parts to one dword per part and stores it (64 lanes: 256 contiguous bytes
+// of a part per instruction).  The next slice's loads are issued before the
+// stores, so one wait covers both.  Wave 15 hashes: lane 4e + a is XXH64
+// accumulator a of part p0 + e; once every encoder wave has stored slice i
+// (its stores complete, then its LDS progress count), the hash wave folds
+// slice i's 120 rounds from the L2.  The encoders never wait for it -- it
+// may still be folding a unit while they encode the next -- and they
+// synchronise among themselves through an LDS counter, so the tables of the
+// next unit need no workgroup barrier.  The parts are read once from HBM
+// (the hash re-read hits the L2).  Units u, u + 8, u + 16 are a stripe's
+// part groups on one XCD (workgroup b runs on XCD b mod 8), side by side:
+// they share the block's lines in its L2.
+constexpr int BE_WAVES = 16, BE_EW = 15;
+constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
+constexpr int BE_CMAX = 32;
+
+// barrier of the encoder waves only (LDS counter; the hash wave runs on)
+__device__ __forceinline__ void enc_barrier(u32 *bar, u32 &gen, int lane)
+{
+    gen += BE_EW;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0)
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// unit u -> stripe (nstripes or more: none) and part group
+__device__ __forceinline__ u32 be_stripe(u32 u, u32 ngroups, u32 &grp)
+{
+    const u32 loc = u >> 3;
+    grp = loc % ngroups;
+    return (loc / ngroups) * 8 + (u & 7);
+}
+
+template <bool HASH, int KC>
+__global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, const u8 *ids, u64 *digests,
+                                                                   u32 ngroups, u32 nunits)
+{
+    __shared__ __attribute__((aligned(16))) u8 tbl[BE_CMAX * 4096];
+    __shared__ u32 done[BE_WAVES];  // slices stored so far, per encoder wave
+    __shared__ u32 bar;
+
+    const int n = g.n, k = g.k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nch = (k + 15) >> 4;
+    if (tid < BE_WAVES)
+        done[tid] = 0;
+    if (tid == 0)
+        bar = 0;
+    __syncthreads();
+
+    if (wave < BE_EW) {
+        u32 gen = 0, seq = 0;
+#pragma unroll 1
+        for (u32 u = blockIdx.x; u < nunits; u += gridDim.x) {
+            u32 grp;
+            const u32 s = be_stripe(u, ngroups, grp);
+            if (s >= g.nstripes)
+                continue;  // the whole workgroup
+            const Stripe v = stripe_at(g, s);
+            const int p0 = int(grp) * 16, np = min(16, n - p0);
+
+            // every encoder wave is done with the previous unit's tables
+            enc_barrier(&bar, gen, lane);
+            // Vandermonde rows of the group's parts, x^m by square and
+            // multiply (crt/nk8.c:404-406 builds the same powers by repeated
+            // multiplication): lane 16t + e computes byte e of the wave's
+            // table t (columns wave, wave + 15, wave + 30), the rows are
+            // gathered into scalars; parts past n and columns past k: 0
+            u32 xb;
+            {
+                const int t = lane >> 4, e = lane & 15, m = wave + BE_EW * t;
+                u32 r = 0;
+                if (e < np && m < k && t < 3) {
+                    u32 x = ids[u64(s) * u64(n) + u64(p0 + e)];
+                    r = 1;
+#pragma unroll
+                    for (int bit = 0; bit < 5; ++bit) {
+                        if ((m >> bit) & 1)
+                            r = gf_mul_packed(r, x);
+                        x = gf_mul_packed(x, x);
+                    }
+                }
+                xb = r;
+            }
+#pragma unroll 1
+            for (int t = 0; t < 3; ++t) {
+                const int m = wave + BE_EW * t;
+                if (m >= 16 * nch)
+                    break;  // uniform
+                if (m < k) {
+                    u32 row[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        u32 r = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            r |= u32(__builtin_amdgcn_readlane(int(xb), 16 * t + 4 * w + i)) << (8 * i);
+                        row[w] = r;
+                    }
+                    u32 basis[8][4];
+                    make_basis<4>(basis, row);
+                    build_table16(tbl + m * 4096, basis, lane);
+                } else {  // columns k .. 16 nch - 1: zero (lookups go in column pairs)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        *reinterpret_cast<uint4 *>(tbl + m * 4096 + (lane + 64 * i) * 16) = make_uint4(0, 0, 0, 0);
+                }
+            }
+            enc_barrier(&bar, gen, lane);
+
+            // the block through a buffer resource based at the dword below
+            // it: loads are dword aligned and anything past B reads 0 (the
+            // bytes past B inside its last dword are masked in the last slice)
+            const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<u8 *>(v.blk - mis), (short)0, int((v.B + mis + 3u) & ~3u), 0x00020000);
+            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 rl = u32(wave * 64 + lane) * 4u;
+            // every chunk's bytes of a slice's 4 rows, all loads in flight at
+            // once: KC (k % 4 == 0, dword-aligned block) the 4k contiguous
+            // bytes of the lane's rows in k/4 16-byte loads; otherwise per
+            // row and chunk a 16 + 4-byte load, aligned by v_alignbyte
+            constexpr int NR = KC ? 1 : 2;
+            u32 raw[NR][4][5];
+            u32 rw[KC ? KC : 1];
+            auto load = [&](u32 r0) {
+                if constexpr (KC) {
+#pragma unroll
+                    for (int i = 0; i < KC / 4; ++i) {
+                        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, r0 * u32(KC) + 16u * u32(i), 0, 0);
+                        rw[4 * i] = x.x;
+                        rw[4 * i + 1] = x.y;
+                        rw[4 * i + 2] = x.z;
+                        rw[4 * i + 3] = x.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (c >= nch)
+                            break;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32 a = ((r0 + u32(q)) * u32(k) + 16u * u32(c) + mis) & ~3u;
+                            const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+                            raw[c][q][0] = x.x;
+                            raw[c][q][1] = x.y;
+                            raw[c][q][2] = x.z;
+                            raw[c][q][3] = x.w;
+                            raw[c][q][4] = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
+                        }
+                    }
+                }
+            };
+            load(rl);
+#pragma unroll 1
+            for (u32 sl = 0; sl < nsl; ++sl) {
+                const u32 r0 = sl * BE_ROWS + rl;
+                const bool last = sl + 1 == nsl;
+                uint4 acc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (c >= nch)
+                        break;
+                    u32 d[4][4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const u32 pos = (r0 + u32(q)) * u32(k) + 16u * u32(c);
+                        if constexpr (KC) {
+                            // dwords past the row's k bytes meet zero tables
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                d[q][w] = 4 * c + w < KC / 4 ? rw[q * (KC / 4) + 4 * c + w] : 0u;
+                        } else {
+                            const u32 sh = (pos + mis) & 3u;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                d[q][w] = __builtin_amdgcn_alignbyte(raw[c % NR][q][w + 1], raw[c % NR][q][w], sh);
+                        }
+                        if (last) {
+                            // bytes at or past B are zero (the reference
+                            // zero-pads its tail row); columns past k meet
+                            // zero tables
+                            const u32 valid = v.B > pos ? min(v.B - pos, 16u) : 0u;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w) {
+                                const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
+                                d[q][w] &= u32((u64(1) << (8 * keep)) - 1u);
+                            }
+                        }
+                    }
+                    // columns in pairs (one three-input XOR per word folds
+                    // both); tdep (0 at run time) keeps 16 lookups in flight
+                    u32 tdep = u32(c) * 65536u;
+#pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        if (16 * c + j >= k)
+                            break;  // uniform
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
+                            const u32 s1 = 0x0C0C0C00u | u32(4 + ((j + 1) & 3));
+                            const u32 P0 = (__builtin_amdgcn_perm(d[q][j >> 2], 0u, s0) << 4) + tdep;
+                            const u32 P1 = (__builtin_amdgcn_perm(d[q][(j + 1) >> 2], 0u, s1) << 4) + tdep;
+                            const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
+                            const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
+                            acc[q].x = xor3(acc[q].x, a.x, c2.x);
+                            acc[q].y = xor3(acc[q].y, a.y, c2.y);
+                            acc[q].z = xor3(acc[q].z, a.z, c2.z);
+                            acc[q].w = xor3(acc[q].w, a.w, c2.w);
+                        }
+                        if (j & 2) {
+                            u32 z;
+                            asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(acc[3].x));
+                            tdep = u32(c) * 65536u + z;
+                        }
+                    }
+                }
+                // the next slice's loads fly under this slice's stores
+                if (!last)
+                    load(r0 + BE_ROWS);
+                // row quad -> one dword of 4 rows per part
+                if (r0 < v.ps) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const u32 *aw0 = &acc[0].x, *aw1 = &acc[1].x, *aw2 = &acc[2].x, *aw3 = &acc[3].x;
+                        u32 o[4];
+                        transpose4(aw0[w], aw1[w], aw2[w], aw3[w], o[0], o[1], o[2], o[3]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int e = 4 * w + i;
+                            if (e >= np)
+                                break;
+                            u8 *dst = v.parts + u64(p0 + e) * v.pitch + r0;
+                            if (r0 + 4u <= v.ps) {
+                                *reinterpret_cast<u32 *>(dst) = o[i];
+                            } else {
+                                for (u32 cb = 0; cb < 4 && r0 + cb < v.ps; ++cb)
+                                    dst[cb] = u8(o[i] >> (8 * cb));
+                            }
+                        }
+                    }
+                }
+                if constexpr (HASH) {
+                    // this slice's stores are complete (in the L2) before
+                    // the progress count the hash wave polls
+                    __builtin_amdgcn_s_waitcnt(0);
+                    ++seq;
+                    if (lane == 0)
+                        __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+    } else if constexpr (HASH) {
+        const int e = lane >> 2, a = lane & 3;
+        u32 seq = 0;
+#pragma unroll 1
+        for (u32 u = blockIdx.x; u < nunits; u += gridDim.x) {
+            u32 grp;
+            const u32 s = be_stripe(u, ngroups, grp);
+            if (s >= g.nstripes)
+                continue;
+            const Stripe v = stripe_at(g, s);
+            const int p0 = int(grp) * 16, np = min(16, n - p0);
+            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
+            // the group's parts through one buffer resource (the launcher
+            // checks n * pitch < 2^31); loads bypass the CU's L1 (sc0)
+            const __amdgpu_buffer_rsrc_t pr =
+                __builtin_amdgcn_make_buffer_rsrc(v.parts, (short)0, int(u64(n) * v.pitch), 0x00020000);
+            const u32 pbase = u32(u64(p0 + min(e, np - 1)) * v.pitch);
+            u64 hacc = xxh_acc_init(a, 0);
+#pragma unroll 1
+            for (u32 sl = 0; sl < nsl; ++sl) {
+                ++seq;
+                for (;;) {
+                    const u32 dv = lane < BE_EW ? __hip_atomic_load(&done[lane], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)
+                                                : 0xFFFFFFFFu;
+                    if (!__ballot(dv < seq))
+                        break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const u32 rb = sl * (BE_ROWS / 32u);
+                const int re = int(min(rb + BE_ROWS / 32u, nst));
+                // a ring of 4 x 8 rounds: three batches' loads in flight
+                // while one is folded (the chain is bound by its serial
+                // rounds, ~35 ns each, not by the L2's latency); loads past
+                // the slice's rounds are never folded
+                auto ld = [&](uint64_t (&w)[8], u32 r) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(
+                            pr, pbase + 32u * (r + u32(i)) + 8u * u32(a), 0, 1);
+                        w[i] = (u64(x.y) << 32) | x.x;
+                    }
+                };
+                uint64_t w0[8], w1[8], w2[8], w3[8];
+                ld(w0, rb);
+                ld(w1, rb + 8);
+                ld(w2, rb + 16);
+#pragma unroll 1
+                for (int r = int(rb); r < re; r += 32) {
+                    ld(w3, u32(r) + 24);
+                    hacc = xxh_rounds<8>(hacc, w0, re - r);
+                    ld(w0, u32(r) + 32);
+                    hacc = xxh_rounds<8>(hacc, w1, re - r - 8);
+                    ld(w1, u32(r) + 40);
+                    hacc = xxh_rounds<8>(hacc, w2, re - r - 16);
+                    ld(w2, u32(r) + 48);
+                    hacc = xxh_rounds<8>(hacc, w3, re - r - 24);
+                }
+            }
+            // every slice is stored: the tail (ps & 31 bytes after the last
+            // whole stripe), converge, length, avalanche
+            uint64_t tw[4] = {0, 0, 0, 0};
+            if (v.ps & 31) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const v2u x = __builtin_amdgcn_raw_buffer_load_b64(pr, pbase + 32u * nst + 8u * u32(i), 0, 1);
+                    tw[i] = (u64(x.y) << 32) | x.x;
+                }
+            }
+            const int base = lane & ~3;
+            const u64 v1 = shfl64(hacc, base), v2 = shfl64(hacc, base + 1);
+            const u64 v3 = shfl64(hacc, base + 2), v4 = shfl64(hacc, base + 3);
+            if (a == 0 && e < np) {
+                u64 h = v.ps >= 32 ? xxh_converge(v1, v2, v3, v4) : XP5;
+                h += v.ps;
+                digests[u64(s) * u64(n) + u64(p0 + e)] = xxh_tail_regs(h, tw, v.ps & 31);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // Decode a uniform or ragged batch with 2 <= k <= 254 from the plan
@@ -472,4 +831,55 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
     case 1: return launch_bign<1>(g, work, status, pal, st);
     default: return launch_bign<2>(g, work, status, pal, st);
     }
+}
+
+// Encode a uniform or ragged batch with k <= 32 on k_encode_bign (XXH64 of
+// every part into digests when non-null), persistent or one workgroup per
+// (stripe, part group).  -ENOSYS when the shape is outside
+// what it handles (the caller takes the column-chunked encoder).
+extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool persist,
+                                hipStream_t st)
+{
+    const int k = g->k, n = g->n;
+    if (k < 2 || k > BE_CMAX || n < k || g->part_min || g->part_max)
+        return -ENOSYS;
+    if (!g->nstripes)
+        return 0;
+    // 4-byte aligned parts and pitch (dword stores); block offsets (rows +
+    // one slice) and a stripe's part span inside 31 bits
+    const u64 ps_max = (u64(g->block_size) + u64(k) - 1) / u64(k);  // ragged: block_size = the largest
+    const u64 pitch_max = g->block_sizes ? (ps_max + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1) : g->part_pitch;
+    if (((reinterpret_cast<uintptr_t>(g->parts) | (g->block_sizes ? 0 : g->part_pitch)) & 3) ||
+        (ps_max + BE_ROWS) * u64(k) + 64 > 0x7FFFFFFFull || u64(n) * pitch_max > 0x7FFFFFFFull)
+        return -ENOSYS;
+    const u64 ngroups = (u64(n) + 15) / 16;
+    const u64 nunits = (u64(g->nstripes) + 7) / 8 * 8 * ngroups;
+    if (nunits > 0x7FFFFFFFull)
+        return -EINVAL;
+    // persist: one resident workgroup per CU (a multiple of 8: unit u stays
+    // on XCD u mod 8); else one workgroup per unit
+    const u64 cus = u64(nkfs_cu_count()) / 8 * 8;
+    const u32 grid = u32(!persist || nunits < cus || !cus ? nunits : cus);
+    // k % 4 == 0 with dword-aligned blocks (uniform batches): a lane's 4
+    // rows in k/4 contiguous 16-byte loads (k-specialised kernels)
+    const bool kc = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->blocks) | g->block_pitch) & 3) == 0;
+    const int kk = kc && (k == 20 || k == 24 || k == 28 || k == 32) ? k : 0;
+    auto go = [&](auto hash, auto kcon) {
+        hipLaunchKernelGGL((k_encode_bign<decltype(hash)::value, decltype(kcon)::value>), dim3(grid),
+                           dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits));
+    };
+    auto pick = [&](auto hash) {
+        switch (kk) {
+        case 20: go(hash, std::integral_constant<int, 20>{}); break;
+        case 24: go(hash, std::integral_constant<int, 24>{}); break;
+        case 28: go(hash, std::integral_constant<int, 28>{}); break;
+        case 32: go(hash, std::integral_constant<int, 32>{}); break;
+        default: go(hash, std::integral_constant<int, 0>{});
+        }
+    };
+    if (digests)
+        pick(std::true_type{});
+    else
+        pick(std::false_type{});
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -671,6 +671,8 @@ extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t 
 extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, hipStream_t st);
 extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int mode,
                                 hipStream_t st);
+extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool persist,
+                                hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
@@ -794,6 +796,14 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     }
     if (rc != -ENOSYS)
         return rc;
+    // 16 < k <= 32 with digests: the stage-free encoder with a hash wave
+    // (nk8_bign.hip; tune enc_bign)
+    const int eb = nkfs_tune_now().enc_bign;
+    if (kern != NKFS_ENC_GENERIC && (eb > 0 || (eb == -1 && digests && g->k > 16 && kern == NKFS_ENC_AUTO))) {
+        rc = nkfs_bign_encode(g, ids, digests, eb != 2, st);
+        if (rc != -ENOSYS)
+            return rc;
+    }
     // n > 8 (or a few big stripes), k <= 16: with digests and a batch that
     // fills the chip (two workgroups of 16 parts per CU), the part-group
     // encoder with XXH64 fused (nk8_wide.hip, k_encode_wide_ws)
@@ -913,13 +923,16 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     // 16-column chunks (nk8_big.hip); pinned GENERIC: thread per row
     // the stage-free decoder (nk8_bign.hip): dec_bign >= 0 pins a table
     // layout for every k > 8; -2 (auto, the default) takes byte tables where
-    // they win: k > 16 (W2 N48K32 1,315 -> 2,082 GB/s, N24K20 926 -> 1,211)
-    // and k % 4 == 0 below 16 (W1 N16K12 3,330 -> 4,296); k = 16 (4,087 /
-    // 3,952) and other k keep the survivor-table decoder
-    // (profiles/r05/ab_bign.txt)
+    // they win: k % 4 == 0 except 16 -- W2 N48K32 1,315 -> 2,082 GB/s,
+    // N24K20 926 -> 1,211, W1 N16K12 3,330 -> 4,296; k = 16 (4,087 / 3,952)
+    // keeps the survivor-table decoder (profiles/r05/ab_bign.txt), and k with
+    // rows not a dword multiple keep the column-chunked one, whose output goes
+    // through an LDS stage (the stage-free one writes such rows bytewise:
+    // N40K17 696 / 413, N40K18 736 / 598, N40K33 524 / 523;
+    // profiles/r05/ab_oddk.txt)
     rc = -ENOSYS;
     if (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG) {
-        const bool auto_pick = t.dec_bign == -2 && (g->k > 16 || (g->k % 4 == 0 && g->k < 16));
+        const bool auto_pick = t.dec_bign == -2 && g->k % 4 == 0 && g->k != 16;
         if (t.dec_bign >= 0 || auto_pick)
             rc = nkfs_bign_decode(g, (const u8 *)work, status, t.dec_bign >= 0 ? t.dec_bign : 0, st);
     }

@@ -1,5 +1,5 @@
-"""GPU parity of the column-chunked kernels for k > 16 (nk8_big.hip,
-NKFS_ENC_BIG / NKFS_DEC_BIG): the default for k > 16, any n <= 255 and
+"""GPU parity of the kernels for k > 16: the column-chunked ones
+(nk8_big.hip, NKFS_ENC_BIG / NKFS_DEC_BIG) for any n <= 255 and
 k <= 254 (crt/nk8.c:13-16; the reference's self test draws k up to 254,
 crt/nk8.c:735-744).
 
@@ -9,7 +9,10 @@ Every case is checked bit-exact against the thread-per-row general kernels
 one and several 16-column chunks, part groups of 16 (the last one partial),
 k = n, k = 254 / n = 255, tails of every size, unaligned ragged offsets,
 one-byte blocks, the small-k shapes pinned to the big kernels, the
-first-k-distinct selection and the -EINVAL stripe.
+first-k-distinct selection and the -EINVAL stripe.  The stage-free encoder
+with a hash wave (nk8_bign.hip, k_encode_bign: the default for 16 < k <= 32
+with digests; tune enc_bign = 1 pins it for every k <= 32, with or without
+digests) is held to the same cases.
 """
 import numpy as np
 import pytest
@@ -58,6 +61,9 @@ def _tuned(**kw):
     (17, 17, 17 * 300 + 5, 7),  # k = n
     (16, 12, 65536, 10),       # k <= 16 pinned to the big kernel
     (8, 5, 4096, 50),          # n <= 8 pinned to the big kernel
+    (24, 20, 65543, 5),        # k % 4 == 0: the stage-free encoder's contiguous row loads, tail row
+    (30, 24, 24 * 4096, 4),
+    (29, 28, 4099, 9),
 ])
 def test_big_encode_matches(L, O, n, k, B, S):
     from nkfs_amd import _lib, batch
@@ -71,11 +77,16 @@ def test_big_encode_matches(L, O, n, k, B, S):
     with _tuned(enc_kernel=_lib.ENC["big"], enc_big_fused=1):  # XXH64 fused, chained over the slices
         p3, d3 = batch.encode(blocks, B, n, k, ids)
     p2, d2 = batch.encode(blocks, B, n, k, ids)  # default dispatch
+    with _tuned(enc_bign=1):  # the stage-free encoder, hash wave and no-digest forms
+        p4, d4 = batch.encode(blocks, B, n, k, ids)
+        p5, _ = batch.encode(blocks, B, n, k, ids, digests=False)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
     assert torch.equal(p0[:, :ps], p3[:, :ps]) and torch.equal(d0, d3)
     assert torch.equal(p0[:, :ps], p2[:, :ps]) and torch.equal(d0, d2)
+    assert torch.equal(p0[:, :ps], p4[:, :ps]) and torch.equal(d0, d4)
+    assert torch.equal(p0[:, :ps], p5[:, :ps])
     got = [u64(x) for x in d1.cpu().tolist()]
     for s in sorted({0, S - 1}):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
@@ -83,7 +94,7 @@ def test_big_encode_matches(L, O, n, k, B, S):
         assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
 
 
-@pytest.mark.parametrize("n,k,gap", [(24, 20, 0), (40, 33, 5), (19, 18, 3)])
+@pytest.mark.parametrize("n,k,gap", [(24, 20, 0), (40, 33, 5), (19, 18, 3), (48, 32, 1)])
 def test_big_encode_ragged(L, O, n, k, gap):
     """Ragged batches (mixed sizes, block offsets unaligned when gap != 0):
     the big kernel equals the general kernel, and the oracle per stripe."""
@@ -102,10 +113,10 @@ def test_big_encode_ragged(L, O, n, k, gap):
         host[boff[s]: boff[s] + B] = synth.stripe_bytes(500 + s, int(B))
     ids_np = synth.batch_ids(len(sizes), n, first=500)
     outs = []
-    for kern, fused in (("generic", 0), ("big", 0), ("big", 1)):
+    for kern, fused, eb in (("generic", 0, 0), ("big", 0, 0), ("big", 1, 0), ("auto", 0, -1), ("auto", 0, 1)):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-        with _tuned(enc_kernel=_lib.ENC[kern], enc_big_fused=fused):
+        with _tuned(enc_kernel=_lib.ENC[kern], enc_big_fused=fused, enc_bign=eb):
             batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts,
                                 dev(poff), dig, int(sizes.max()))
         torch.cuda.synchronize()
@@ -177,22 +188,24 @@ def test_big_decode_matches(L, O, n, k, B, S):
 
 
 def test_big_round_trip_w2(L, O):
-    """The bench's W2 batch (256 x 1 MiB, N48K32): the encoder with XXH64
-    fused (each slice continuing its part group's chains from the previous
-    slice's workgroup) gives the same parts and digests as the default one
-    with the separate hash pass, the oracle's digests on a sample; keep 32
-    seeded survivors -> default decode gives every block back."""
+    """The bench's W2 batch (256 x 1 MiB, N48K32): the default encoder (the
+    stage-free one with its hash wave), the column-chunked one with the
+    separate hash pass and with XXH64 fused (each slice continuing its part
+    group's chains from the previous slice's workgroup) give the same parts
+    and digests, the oracle's digests on a sample; keep 32 seeded survivors
+    -> default decode gives every block back."""
     from nkfs_amd import _lib, batch
     S, B, n, k = 256, 1048576, 48, 32
     blocks = batch.synth(S, B, first=11)
     ids_np = synth.batch_ids(S, n, first=11)
     ids = dev(ids_np)
     parts, dig = batch.encode(blocks, B, n, k, ids)
-    with _tuned(enc_big_fused=1 - _lib.get_tune().enc_big_fused):
-        parts1, dig1 = batch.encode(blocks, B, n, k, ids)
-    torch.cuda.synchronize()
-    assert torch.equal(parts, parts1) and torch.equal(dig, dig1)
-    del parts1
+    for fused in (0, 1):
+        with _tuned(enc_bign=0, enc_big_fused=fused):
+            parts1, dig1 = batch.encode(blocks, B, n, k, ids)
+        torch.cuda.synchronize()
+        assert torch.equal(parts, parts1) and torch.equal(dig, dig1), fused
+        del parts1
     got = [u64(x) for x in dig.cpu().tolist()]
     for s in (0, 137, S - 1):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
