@@ -112,6 +112,9 @@ struct nkfs_tune {
 	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64
 	                         pass), 1 = every k <= 32 batch it accepts, persistent (a workgroup per CU walking
 	                         the (stripe, part group) units), 2 = the same, one workgroup per unit */
+	int dec_pair_pipe;    /* k = 2 decode of uniform batches of blocks <= 4 KiB (C2): waves per CU of the persistent
+	                         pipelined pair decoder (next stripes' slots, ids and parts in flight under the current
+	                         one), taken automatically when > 0; 0 = the wave decoder */
 };
 void nkfs_tune_get(struct nkfs_tune *t);    /* copies under a lock: thread-safe */
 int nkfs_tune_set(const struct nkfs_tune *t); /* -EINVAL on out-of-range fields; thread-safe */

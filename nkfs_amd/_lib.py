@@ -37,7 +37,8 @@ class Tune(C.Structure):
                                        "enc_fused_waves_per_cu", "dec_wave_waves_per_cu", "dec_run_units",
                                        "enc_ws_prefetch", "enc_big_fused", "dec_pair_stage",
                                        "host_depth", "host_lanes", "enc_ragged_split", "enc_ws_waves",
-                                       "dec_pair_waves", "enc_few_max", "enc_ws_hash_waves", "enc_persist", "dec_bign", "enc_bign")]
+                                       "dec_pair_waves", "enc_few_max", "enc_ws_hash_waves", "enc_persist", "dec_bign", "enc_bign",
+                                       "dec_pair_pipe")]
 
 
 ENC = {"auto": 0, "walk": 1, "fused": 2, "ws": 3, "generic": 4, "wide": 5, "big": 6, "wide_ws": 7, "wsp": 8}

@@ -679,7 +679,8 @@ extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids,
                                  void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                  hipStream_t st);
 extern "C" int nkfs_pair_decode(const nkfs_geom *g, int n_slots, const uint8_t *ids, const uint8_t *avail,
-                                int navail, int32_t *status, const void *gf, int xp, int waves, hipStream_t st);
+                                int navail, int32_t *status, const void *gf, int xp, int waves, int pipe,
+                                hipStream_t st);
 extern "C" int nkfs_run_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
                                void *work, int32_t *status, const void *gf, int units, int waves, int cus,
                                hipStream_t st);
@@ -879,14 +880,18 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
         // several chunks per wave; the host pipeline's sub-batches (tens of
         // stripes) keep the slice grid (C5 GET from host memory: run 20.7,
         // slice 31.6 GiB/s; profiles/r03/pcie.txt)
+        // dec_pair_pipe > 0: uniform k = 2 batches of blocks up to 4 KiB on
+        // the persistent pipelined pair decoder
+        const bool pipe2 = g->k == 2 && !g->block_sizes && g->block_size <= 4096 && t.dec_pair_pipe > 0;
         const int kern = t.dec_kernel != NKFS_DEC_AUTO         ? t.dec_kernel
+                         : pipe2 && !expect                    ? NKFS_DEC_PAIR
                          : small_k2                            ? NKFS_DEC_WAVE
                          : g->block_sizes && g->nstripes >= 2048 ? NKFS_DEC_RUN
                                                                  : NKFS_DEC_SLICE;
         if (kern == NKFS_DEC_PAIR && !expect) {
             auto pair = [&](const nkfs_geom *go) {
                 return nkfs_pair_decode(go, n_slots, ids, avail, navail, status, gf, t.dec_pair_stage,
-                                        t.dec_pair_waves, st);
+                                        t.dec_pair_waves, t.dec_pair_pipe, st);
             };
             rc = with_size_order(g, st, pair);
             if (rc == -ENOSYS)

@@ -70,6 +70,7 @@ static struct nkfs_tune g_tune = {
 	.enc_persist = 1, /* ragged n > 4: C5 encode 4,839 -> 5,051 GB/s (profiles/r05/ab_wsp.txt) */
 	.dec_bign = -2, /* auto: byte tables for k > 16 and k = 12 (profiles/r05/ab_bign.txt) */
 	.enc_bign = -1,
+	.dec_pair_pipe = 0,
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
 
@@ -100,7 +101,8 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||
 	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2 ||
 	    t->enc_persist < 0 || t->enc_persist > 2 ||
-	    t->dec_bign < -2 || t->dec_bign > 2 || t->enc_bign < -1 || t->enc_bign > 2)
+	    t->dec_bign < -2 || t->dec_bign > 2 || t->enc_bign < -1 || t->enc_bign > 2 ||
+	    t->dec_pair_pipe < 0 || t->dec_pair_pipe > 32)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);
 	g_tune = *t;

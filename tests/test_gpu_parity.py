@@ -938,7 +938,8 @@ def test_pair_decode_matches(L, O, n, B, S):
     offer repeating the first one's id (the selection takes the next distinct
     one, crt/nk8.c:512-537), stripe 2 offering a single distinct id (status
     -EINVAL, block untouched); odd block sizes and tails of every length, long
-    stripes split into row slices."""
+    stripes split into row slices; the persistent pipelined form
+    (dec_pair_pipe) on the shapes it takes."""
     from nkfs_amd import batch
     k = 2
     blocks = batch.synth(S, B, first=21)
@@ -951,8 +952,11 @@ def test_pair_decode_matches(L, O, n, B, S):
         ids2[1, av[1, 1]] = ids2[1, av[1, 0]]
         ids2[2, :] = ids2[2, 0]
     outs = []
-    for kern, stage, waves in (("wave", 1, 4), ("pair", 1, 4), ("pair", 0, 1), ("pair", 1, 1), ("pair", 0, 4)):
-        with _tuned(dec_kernel=_dec(kern), dec_pair_stage=stage, dec_pair_waves=waves):
+    # pipe > 0: the persistent pipelined form (uniform blocks <= 4 KiB; 2
+    # waves per CU: 512 waves walking 5-6 stripes each on the 3,000-stripe case)
+    for kern, stage, waves, pipe in (("wave", 1, 4, 0), ("pair", 1, 4, 0), ("pair", 0, 1, 0), ("pair", 1, 1, 0),
+                                     ("pair", 0, 4, 0), ("pair", 1, 1, 2), ("pair", 0, 1, 2), ("auto", 1, 1, 16)):
+        with _tuned(dec_kernel=_dec(kern), dec_pair_stage=stage, dec_pair_waves=waves, dec_pair_pipe=pipe):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
             torch.cuda.synchronize()
