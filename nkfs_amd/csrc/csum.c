@@ -185,6 +185,135 @@ static int xh_stage(struct xh *h, const uint8_t *p, uint64_t bytes)
 	return 0;
 }
 
+/* ------------------------------------------- per-call service wave (opt-in)
+ *
+ * nkfs_percall_service(1) keeps one wave resident (k_xxh64_service) polling
+ * a mailbox in coherent host memory: a message digested in one piece (no
+ * earlier fold) is posted there instead of launched -- arguments, then the
+ * request number -- and the host spins on the message's completion word as
+ * before.  Requests are serialised by g_svc_lock (one box).  The wave leaves
+ * after SVC_IDLE without requests (or SVC_LIFE in all); a request that finds
+ * it gone, or that it never took, relaunches it once the service stream has
+ * drained. */
+#define SVC_IDLE 2000000ull      /* s_memrealtime ticks (100 MHz): 20 ms */
+#define SVC_LIFE 1000000000ull   /* 10 s */
+static pthread_mutex_t g_svc_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct nkfs_svc_box *g_svc; /* coherent host memory */
+static struct nkfs_svc_box *g_svc_dev_ptr;
+static hipStream_t g_svc_stream;
+static int g_svc_on, g_svc_device = -1, g_svc_exit_hooked;
+
+/* at exit: post a stop and give the wave a bounded time to leave (host
+ * memory only: no runtime calls while the process tears down) */
+static void svc_atexit(void)
+{
+	if (!g_svc || !__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE))
+		return;
+	g_svc->op = NKFS_SVC_STOP;
+	__atomic_store_n(&g_svc->seq, g_svc->seq + 1, __ATOMIC_RELEASE);
+	struct timespec t0, t;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	do {
+		if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE))
+			return;
+		clock_gettime(CLOCK_MONOTONIC, &t);
+	} while ((t.tv_sec - t0.tv_sec) * 1000000000ll + (t.tv_nsec - t0.tv_nsec) < 100000000ll);
+}
+
+static int svc_launch_locked(void)
+{
+	__atomic_store_n(&g_svc->alive, 1, __ATOMIC_RELEASE);
+	int err = nkfs_launch_xxh64_service(g_svc_dev_ptr, SVC_IDLE, SVC_LIFE, g_svc_stream);
+	if (err)
+		__atomic_store_n(&g_svc->alive, 0, __ATOMIC_RELEASE);
+	return err;
+}
+
+int nkfs_percall_service(int on)
+{
+	if (on && ensure_gpu())
+		return -ENODEV;
+	pthread_mutex_lock(&g_svc_lock);
+	int err = 0;
+	if (!on) {
+		if (g_svc && __atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE)) {
+			g_svc->op = NKFS_SVC_STOP;
+			__atomic_store_n(&g_svc->seq, g_svc->seq + 1, __ATOMIC_RELEASE);
+			if (hipStreamSynchronize(g_svc_stream) != hipSuccess)
+				err = -EIO;
+		}
+		__atomic_store_n(&g_svc_on, 0, __ATOMIC_RELEASE);
+		pthread_mutex_unlock(&g_svc_lock);
+		return err;
+	}
+	if (!g_svc) {
+		void *p = NULL, *dp = NULL;
+		if (hipHostMalloc(&p, sizeof(*g_svc), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+			err = -ENOMEM;
+			goto out;
+		}
+		if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess ||
+		    hipStreamCreateWithFlags(&g_svc_stream, hipStreamNonBlocking) != hipSuccess) {
+			(void)hipHostFree(p);
+			err = -EIO;
+			goto out;
+		}
+		memset(p, 0, sizeof(*g_svc));
+		g_svc = p;
+		g_svc_dev_ptr = dp;
+		(void)hipGetDevice(&g_svc_device);
+		if (!g_svc_exit_hooked) {
+			g_svc_exit_hooked = 1;
+			atexit(svc_atexit);
+		}
+	}
+	__atomic_store_n(&g_svc_on, 1, __ATOMIC_RELEASE);
+out:
+	pthread_mutex_unlock(&g_svc_lock);
+	return err;
+}
+
+/* Run one message on the service wave and wait for its completion word;
+ * -ENOSYS when the service is off (or on another device): launch instead. */
+static int svc_run(const struct nkfs_xxh_args *a, volatile uint64_t *res)
+{
+	if (!__atomic_load_n(&g_svc_on, __ATOMIC_ACQUIRE))
+		return -ENOSYS;
+	int dev = -1;
+	(void)hipGetDevice(&dev);
+	pthread_mutex_lock(&g_svc_lock);
+	if (!g_svc_on || dev != g_svc_device) {
+		pthread_mutex_unlock(&g_svc_lock);
+		return -ENOSYS;
+	}
+	int err = 0;
+	if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
+	    (err = svc_launch_locked()))
+		goto out;
+	g_svc->op = NKFS_SVC_XXH;
+	g_svc->args = *a;
+	const uint64_t sq = g_svc->seq + 1;
+	__atomic_store_n(&g_svc->seq, sq, __ATOMIC_RELEASE);
+	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag; spin++) {
+		if ((spin & 0xFFF) == 0xFFF && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) != sq &&
+		    !__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE)) {
+			/* the wave left without taking the request: relaunch once it is gone */
+			hipError_t q = hipStreamQuery(g_svc_stream);
+			if (q == hipSuccess) {
+				if ((err = svc_launch_locked()))
+					goto out;
+			} else if (q != hipErrorNotReady) {
+				err = -EIO;
+				goto out;
+			}
+		}
+		__builtin_ia32_pause();
+	}
+out:
+	pthread_mutex_unlock(&g_svc_lock);
+	return err;
+}
+
 /* Launch the last fold with `flags` (EMIT / FINISH) and wait for its
  * completion word: a spin on pinned memory, with the stream's own status
  * checked now and then so a failed launch cannot spin forever. */
@@ -201,7 +330,14 @@ static int xh_complete(struct xh *h, uint32_t flags, const struct xstate *s, uin
 	volatile uint64_t *res = (volatile uint64_t *)h->res;
 	a.flag = ++h->c->seq | (1ull << 63);
 	res[1] = 0;
-	int err = nkfs_launch_xxh64_chain(&a, h->c->stream);
+	/* a message in one piece may go to the resident service wave */
+	int err = h->folded ? -ENOSYS : svc_run(&a, res);
+	if (err != -ENOSYS) {
+		if (err)
+			return err;
+		goto done;
+	}
+	err = nkfs_launch_xxh64_chain(&a, h->c->stream);
 	if (err)
 		return err;
 	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a.flag; spin++) {
@@ -214,6 +350,7 @@ static int xh_complete(struct xh *h, uint32_t flags, const struct xstate *s, uin
 		}
 		__builtin_ia32_pause();
 	}
+done:
 	if (digest)
 		*digest = res[0];
 	if (v)

@@ -104,6 +104,20 @@ struct nkfs_xxh_args {
 	uint32_t flags;
 };
 int nkfs_launch_xxh64_chain(const struct nkfs_xxh_args *a, void *stream);
+/* Mailbox of the per-call service wave (k_xxh64_service), in coherent host
+ * memory: the host writes op and args, then seq (release); the wave copies
+ * the args, stores taken = seq, runs the message and stores its completion
+ * word; alive drops to 0 when the wave leaves. */
+#define NKFS_SVC_XXH 1u
+#define NKFS_SVC_STOP 2u
+struct nkfs_svc_box {
+	uint64_t seq;
+	uint64_t op;
+	struct nkfs_xxh_args args;
+	uint64_t taken;
+	uint64_t alive;
+};
+int nkfs_launch_xxh64_service(struct nkfs_svc_box *mb, uint64_t idle_ticks, uint64_t life_ticks, void *stream);
 int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 			    const uint64_t *len, uint32_t count, uint64_t seed,
 			    uint64_t *out, void *stream);

@@ -40,9 +40,8 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // and runs its 32 rounds.
 constexpr int NS = 32;
 
-__global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
+__device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring)
 {
-    __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
     const int li = threadIdx.x, lane = li & 3;
     // (selects, not a.v[lane]: a dynamically indexed kernel argument goes
     // through scratch)
@@ -61,14 +60,22 @@ __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
                                          0, 0);
     };
     if (nst) {
+        // only the message's own slots are fetched (a short message is one
+        // PCIe round trip, not NS KiB of ring fill); the last NS - 1 slots
+        // are waited for together
 #pragma unroll
         for (int c = 0; c < NS - 1; ++c)
-            issue(u64(c));
+            if (u64(c) < nslots)
+                issue(u64(c));
         // full slots: no per-round select on the chain's critical path
         const u64 nfull = nst / 32;
         for (u64 c = 0; c < nslots; ++c) {
-            issue(c + NS - 1);  // into the slot slot c-1 was read from
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+            if (c + NS - 1 < nslots) {
+                issue(c + NS - 1);  // into the slot slot c-1 was read from
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             // The multiplies by P2 do not depend on the chain: all 64 lanes
             // take them for the whole slot (two words each, in place), so
             // the four chain lanes' rounds are add, rotate, multiply by P1.
@@ -146,6 +153,49 @@ __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
     __hip_atomic_store(a.out + 1, a.flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
+{
+    __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
+    chain_run(a, ring);
+}
+
+// The opt-in resident service (nkfs_percall_service): one wave polls a
+// mailbox in fine-grained (coherent) host memory and runs each posted
+// message exactly as k_xxh64_chain would, so a per-call digest needs no
+// kernel launch -- the host writes the arguments, then the request number,
+// and spins on the message's own completion word as before.  The wave leaves
+// after `idle` ticks (s_memrealtime, 100 MHz) without a request, after
+// `life` ticks in all, or on a stop request, and clears `alive` as it goes:
+// no schedule can leave it running, and the host relaunches it when a
+// request finds it gone.
+__global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle, u64 life)
+{
+    __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
+    u64 last = __hip_atomic_load(&mb->taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    u64 tl = t0;
+    for (;;) {
+        const u64 sq = __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sq != last) {
+            last = sq;
+            if (mb->op != NKFS_SVC_XXH)
+                break;  // stop
+            const nkfs_xxh_args a = mb->args;
+            if (threadIdx.x == 0)  // the arguments are taken: the box may be reused
+                __hip_atomic_store(&mb->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            chain_run(a, ring);
+            tl = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
+        const u64 now = __builtin_amdgcn_s_memrealtime();
+        if (now - tl > idle || now - t0 > life)
+            break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&mb->alive, u64(0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 extern "C" int nkfs_launch_xxh64_chain(const nkfs_xxh_args *a, void *stream)
@@ -154,5 +204,13 @@ extern "C" int nkfs_launch_xxh64_chain(const nkfs_xxh_args *a, void *stream)
         ((a->flags & (NKFS_XXH_FINISH | NKFS_XXH_EMIT)) && !a->out) || a->tail_len > 31)
         return -EINVAL;
     hipLaunchKernelGGL(k_xxh64_chain, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int nkfs_launch_xxh64_service(nkfs_svc_box *mb, uint64_t idle_ticks, uint64_t life_ticks, void *stream)
+{
+    if (!mb)
+        return -EINVAL;
+    hipLaunchKernelGGL(k_xxh64_service, dim3(1), dim3(64), 0, (hipStream_t)stream, mb, idle_ticks, life_ticks);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -193,3 +193,47 @@ def test_concurrent_digests_of_one_state(L, O):
             t.join()
         assert got == [O.xxh64(a)] * 4, trial
         L.XXH64_freeState(st)
+
+
+def test_percall_service(L, O):
+    """The opt-in resident service wave (nkfs_percall_service, k_xxh64_service):
+    one-piece messages are posted to its host-memory mailbox instead of
+    launched; longer ones (an earlier 256 KiB fold) keep the launch path.
+    Digests match the oracle across lengths and seeds, from eight threads at
+    once (requests serialised on the one mailbox), after the wave left on its
+    20 ms idle timeout (the next request relaunches it), and after the
+    service is switched off again."""
+    import time
+    from nkfs_amd import crt
+    rng = np.random.default_rng(31)
+    assert L.nkfs_percall_service(1) == 0
+    try:
+        for n in [0, 1, 31, 32, 64, 1000, 65536, 262144, 262144 + 33, 700001]:
+            for seed in (0, 5):
+                data = rng.integers(0, 256, n, dtype=np.uint8)
+                assert crt.xxh64(data, seed) == O.xxh64(data, seed), (n, seed)
+        time.sleep(0.1)  # past the idle timeout: the wave has left
+        data = rng.integers(0, 256, 4096, dtype=np.uint8)
+        assert crt.xxh64(data) == O.xxh64(data)
+        cs = crt.Csum()
+        cs.update(data[:10])
+        cs.update(data[10:])
+        assert cs.digest() == O.xxh64(data)
+        datas = [rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8) for _ in range(256)]
+        want = [O.xxh64(d) for d in datas]
+        got = [None] * len(datas)
+
+        def work(t):
+            for i in range(t, len(datas), 8):
+                got[i] = crt.xxh64(datas[i])
+
+        th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert got == want
+    finally:
+        assert L.nkfs_percall_service(0) == 0
+    data = rng.integers(0, 256, 777, dtype=np.uint8)
+    assert crt.xxh64(data) == O.xxh64(data)

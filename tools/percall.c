@@ -93,6 +93,15 @@ int main(int argc, char **argv)
 		fprintf(stderr, "nk8_init failed\n");
 		return 1;
 	}
+	/* PERCALL_SVC=1: the product's opt-in resident service wave for the
+	 * per-call digests (nkfs_percall_service; absent in the reference) */
+	if (getenv("PERCALL_SVC")) {
+		int (*svc)(int) = (int (*)(int))dlsym(h, "nkfs_percall_service");
+		if (!svc || svc(1)) {
+			fprintf(stderr, "nkfs_percall_service unavailable\n");
+			return 1;
+		}
+	}
 	const size_t maxb = 1u << 20;
 	uint8_t *buf = malloc(maxb), *out = malloc(maxb);
 	for (size_t i = 0; i < maxb; i++)
