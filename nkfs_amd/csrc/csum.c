@@ -35,6 +35,7 @@
  */
 #include <errno.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -275,7 +276,27 @@ out:
 
 /* Run one message on the service wave and wait for its completion word;
  * -ENOSYS when the service is off (or on another device): launch instead. */
-static int svc_run(const struct nkfs_xxh_args *a, volatile uint64_t *res)
+/* NKFS_SVC_TRACE=1: per-request phase times of the service path, printed
+ * at exit (post -> the wave took the request -> completion word seen) */
+static int g_svc_trace = -1;
+static double g_tr_take, g_tr_done;
+static uint64_t g_tr_n;
+
+static double mono_us(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static void svc_trace_report(void)
+{
+	if (g_tr_n)
+		fprintf(stderr, "nkfs svc trace: %llu requests, post->taken %.2f us, taken->done %.2f us (means)\n",
+			(unsigned long long)g_tr_n, g_tr_take / g_tr_n, g_tr_done / g_tr_n);
+}
+
+static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile uint64_t *res)
 {
 	if (!__atomic_load_n(&g_svc_on, __ATOMIC_ACQUIRE))
 		return -ENOSYS;
@@ -290,11 +311,28 @@ static int svc_run(const struct nkfs_xxh_args *a, volatile uint64_t *res)
 	if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
 	    (err = svc_launch_locked()))
 		goto out;
-	g_svc->op = NKFS_SVC_XXH;
 	g_svc->args = *a;
+	/* a message of at most 1 KiB of stripes travels inline: the wave reads
+	 * it in the same round trip as the arguments */
+	if (a->nst * 32 <= NKFS_SVC_INL) {
+		memcpy(g_svc->inl, hsrc, a->nst * 32);
+		g_svc->args.src = g_svc_dev_ptr->inl;
+		g_svc->op = NKFS_SVC_XXH_INL;
+	} else {
+		g_svc->op = NKFS_SVC_XXH;
+	}
 	const uint64_t sq = g_svc->seq + 1;
+	if (g_svc_trace < 0) {
+		g_svc_trace = getenv("NKFS_SVC_TRACE") != NULL;
+		if (g_svc_trace)
+			atexit(svc_trace_report);
+	}
+	const double t0 = g_svc_trace ? mono_us() : 0;
+	double t1 = 0;
 	__atomic_store_n(&g_svc->seq, sq, __ATOMIC_RELEASE);
 	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag; spin++) {
+		if (g_svc_trace && !t1 && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) == sq)
+			t1 = mono_us();
 		if ((spin & 0xFFF) == 0xFFF && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) != sq &&
 		    !__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE)) {
 			/* the wave left without taking the request: relaunch once it is gone */
@@ -308,6 +346,14 @@ static int svc_run(const struct nkfs_xxh_args *a, volatile uint64_t *res)
 			}
 		}
 		__builtin_ia32_pause();
+	}
+	if (g_svc_trace) {
+		const double t2 = mono_us();
+		if (!t1)
+			t1 = t2;
+		g_tr_take += t1 - t0;
+		g_tr_done += t2 - t1;
+		g_tr_n++;
 	}
 out:
 	pthread_mutex_unlock(&g_svc_lock);
@@ -331,7 +377,7 @@ static int xh_complete(struct xh *h, uint32_t flags, const struct xstate *s, uin
 	a.flag = ++h->c->seq | (1ull << 63);
 	res[1] = 0;
 	/* a message in one piece may go to the resident service wave */
-	int err = h->folded ? -ENOSYS : svc_run(&a, res);
+	int err = h->folded ? -ENOSYS : svc_run(&a, h->stage[h->cur], res);
 	if (err != -ENOSYS) {
 		if (err)
 			return err;

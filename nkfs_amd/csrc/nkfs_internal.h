@@ -110,12 +110,15 @@ int nkfs_launch_xxh64_chain(const struct nkfs_xxh_args *a, void *stream);
  * word; alive drops to 0 when the wave leaves. */
 #define NKFS_SVC_XXH 1u
 #define NKFS_SVC_STOP 2u
+#define NKFS_SVC_XXH_INL 3u  /* the message's stripes (<= 1 KiB) are in inl */
+#define NKFS_SVC_INL 1024u
 struct nkfs_svc_box {
 	uint64_t seq;
 	uint64_t op;
 	struct nkfs_xxh_args args;
 	uint64_t taken;
 	uint64_t alive;
+	uint8_t inl[NKFS_SVC_INL] __attribute__((aligned(64)));
 };
 int nkfs_launch_xxh64_service(struct nkfs_svc_box *mb, uint64_t idle_ticks, uint64_t life_ticks, void *stream);
 int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,

@@ -40,7 +40,9 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // and runs its 32 rounds.
 constexpr int NS = 32;
 
-__device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring)
+// pre: slot 0 (a message of at most 32 stripes) is already in flight into
+// ring slot 0 (the service wave's inline read)
+__device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring, bool pre = false)
 {
     const int li = threadIdx.x, lane = li & 3;
     // (selects, not a.v[lane]: a dynamically indexed kernel argument goes
@@ -65,7 +67,7 @@ __device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring)
         // are waited for together
 #pragma unroll
         for (int c = 0; c < NS - 1; ++c)
-            if (u64(c) < nslots)
+            if (u64(c) < nslots && !(pre && c == 0))
                 issue(u64(c));
         // full slots: no per-round select on the chain's critical path
         const u64 nfull = nst / 32;
@@ -178,12 +180,23 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle
         const u64 sq = __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (sq != last) {
             last = sq;
-            if (mb->op != NKFS_SVC_XXH)
+            // the inline message bytes (up to 1 KiB) into ring slot 0 in the
+            // same round trip as the arguments
+            __builtin_amdgcn_global_load_lds((const void *)(mb->inl + 16 * threadIdx.x),
+                                             (__attribute__((address_space(3))) void *)ring, 16, 0, 0);
+            const u64 op = mb->op;
+            if (op != NKFS_SVC_XXH && op != NKFS_SVC_XXH_INL) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 break;  // stop
-            const nkfs_xxh_args a = mb->args;
+            }
+            nkfs_xxh_args a = mb->args;
+            const bool inl = op == NKFS_SVC_XXH_INL;
+            if (!inl)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unused inline read lands first
             if (threadIdx.x == 0)  // the arguments are taken: the box may be reused
                 __hip_atomic_store(&mb->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            chain_run(a, ring);
+            chain_run(a, ring, inl);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a message under 32 B left the inline read unused)
             tl = __builtin_amdgcn_s_memrealtime();
             continue;
         }
