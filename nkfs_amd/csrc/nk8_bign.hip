@@ -477,6 +477,15 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 // (the hash re-read hits the L2).  Units u, u + 8, u + 16 are a stripe's
 // part groups on one XCD (workgroup b runs on XCD b mod 8), side by side:
 // they share the block's lines in its L2.
+// NKFS_BE_SLC=1 (experiment builds): the block loads non-temporal (slc)
+#ifndef NKFS_BE_SLC
+#define NKFS_BE_SLC 0
+#endif
+// NKFS_BE_SLICE_BAR=1 (experiment builds): the encoder waves meet after every
+// slice, bounding how long a slice's parts wait in the L2 for the hash wave
+#ifndef NKFS_BE_SLICE_BAR
+#define NKFS_BE_SLICE_BAR 0
+#endif
 constexpr int BE_WAVES = 16, BE_EW = 15;
 constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
 constexpr int BE_CMAX = 32;
@@ -597,7 +606,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 if constexpr (KC) {
 #pragma unroll
                     for (int i = 0; i < KC / 4; ++i) {
-                        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, r0 * u32(KC) + 16u * u32(i), 0, 0);
+                        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, r0 * u32(KC) + 16u * u32(i), 0,
+                                                                            NKFS_BE_SLC ? 2 : 0);
                         rw[4 * i] = x.x;
                         rw[4 * i + 1] = x.y;
                         rw[4 * i + 2] = x.z;
@@ -720,6 +730,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     ++seq;
                     if (lane == 0)
                         __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (NKFS_BE_SLICE_BAR)
+                        enc_barrier(&bar, gen, lane);
                 }
             }
         }

@@ -8,5 +8,5 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 obj=/tmp/ab_obj_$name
 rm -rf "$obj" && cp -a "$root/nkfs_amd/build" "$obj"
 for f in "$@"; do rm -f "$obj/${f%.hip}.o"; done
-make -s -C "$root/nkfs_amd/csrc" OUTDIR="$root/ab_libs/$name" OBJDIR="$obj" EXTRA_HIPFLAGS="$flags"
+make -s -C "$root/nkfs_amd/csrc" OUTDIR="$root/ab_libs/$name" OBJDIR="$obj" BASEOBJ="$obj" EXTRA_HIPFLAGS="$flags"
 echo "built ab_libs/$name/libnkfs_crt.so"
