@@ -725,8 +725,12 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 }
                 if constexpr (HASH) {
                     // this slice's stores are complete (in the L2) before
-                    // the progress count the hash wave polls
-                    __builtin_amdgcn_s_waitcnt(0);
+                    // the progress count the hash wave polls: a release
+                    // fence orders them for the compiler (the s_waitcnt
+                    // builtin alone does not: stores could sink below it),
+                    // the asm wait for the hardware
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     ++seq;
                     if (lane == 0)
                         __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -770,13 +774,17 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 const int re = int(min(rb + BE_ROWS / 32u, nst));
                 // a ring of 4 x 8 rounds: three batches' loads in flight
                 // while one is folded (the chain is bound by its serial
-                // rounds, ~35 ns each, not by the L2's latency); loads past
-                // the slice's rounds are never folded
+                // rounds, ~35 ns each, not by the L2's latency).  Loads past
+                // the slice's rounds are never folded and re-read its last
+                // round: rows of the next slice are not stored yet, and a
+                // line fetched early could still sit in the CU's L1 when
+                // that slice is folded
+                const u32 rlast = re > int(rb) ? u32(re) - 1u : rb;
                 auto ld = [&](uint64_t (&w)[8], u32 r) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(
-                            pr, pbase + 32u * (r + u32(i)) + 8u * u32(a), 0, 1);
+                        const u32 ri = min(r + u32(i), rlast);
+                        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(pr, pbase + 32u * ri + 8u * u32(a), 0, 1);
                         w[i] = (u64(x.y) << 32) | x.x;
                     }
                 };
