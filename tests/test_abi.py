@@ -251,3 +251,29 @@ def test_host_lane_plan_interleaves_devices():
     assert len(p) == 16 and set(p) == set(range(10))
     assert plan(list(range(4)), 4) == [0, 1, 2, 3] * 4
     assert plan([], 2) == [] and plan([3], 0) == [3]
+
+
+def test_tune_struct_and_ranges():
+    """struct nkfs_tune (include/nkfs_gpu.h) and its ctypes mirror have the
+    same int fields in the same order, the round-5 defaults are the measured
+    ones, and nkfs_tune_set rejects out-of-range values (-EINVAL, the state
+    unchanged).  CPU only: the tune state needs no device."""
+    import os
+    import re
+    from conftest import ROOT
+    hdr = open(os.path.join(ROOT, "include", "nkfs_gpu.h")).read()
+    body = hdr[hdr.index("struct nkfs_tune {"): hdr.index("};", hdr.index("struct nkfs_tune {"))]
+    names = re.findall(r"^\s*int\s+(\w+);", body, re.M)
+    assert names == [f for f, _ in _lib.Tune._fields_]
+    t0 = _lib.get_tune()
+    assert (t0.enc_persist, t0.dec_bign, t0.enc_bign, t0.dec_pair_pipe) == (1, -2, -1, 0)
+    L = _lib.lib()
+    for field, bad, good in (("enc_bign", 3, 2), ("enc_bign", -2, 0), ("dec_pair_pipe", 33, 8),
+                             ("dec_pair_pipe", -1, 0), ("dec_bign", 3, 1), ("enc_persist", 3, 2)):
+        t = _lib.get_tune()
+        setattr(t, field, bad)
+        assert L.nkfs_tune_set(C.byref(t)) == -22, field
+        assert getattr(_lib.get_tune(), field) == getattr(t0, field)
+        setattr(t, field, good)
+        assert L.nkfs_tune_set(C.byref(t)) == 0, field
+        assert L.nkfs_tune_set(C.byref(t0)) == 0
