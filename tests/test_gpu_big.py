@@ -222,3 +222,41 @@ def test_big_round_trip_w2(L, O):
         assert int(status2.abs().sum()) == 0 and torch.equal(out2, out), mode
         del out2
     assert torch.equal(out, blocks[:, :B])
+
+
+@pytest.mark.parametrize("gap", [0, 1])
+def test_bign_hash_handoff_repeated(L, gap):
+    """The stage-free encoder's hash wave folds each slice from the L2 after
+    every encoder wave published its progress count; a hand-off that let it
+    read rows before they were visible gave one part group wrong digests in
+    a few runs out of ten (round 5, an LDS capture variant, reverted).  Ten
+    launches of a ragged N48K32 batch per block alignment: every digest
+    equal to the column-chunked kernel's + hash pass."""
+    from nkfs_amd import batch
+    n, k = 48, 32
+    sizes = synth.mixed_sizes(16)
+    sizes[:5] = (4096, 65536, 1048576, 1, k + 1)
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos = ppos = 0
+    for s, B in enumerate(sizes):
+        boff[s], poff[s] = pos, ppos
+        pos += int(B) + gap
+        ppos += n * batch.part_pitch(int(B), k)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(900 + s, int(B))
+    ids = dev(synth.batch_ids(len(sizes), n, first=900))
+    args = (dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, ids)
+    ref = None
+    for run in range(11):
+        parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+        dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+        with _tuned(enc_bign=0 if run == 0 else -1):
+            batch.encode_ragged(*args, parts, dev(poff), dig, int(sizes.max()))
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = (parts.clone(), dig.clone())
+        else:
+            bad = (dig != ref[1]).nonzero().flatten().tolist()
+            assert not bad and torch.equal(parts, ref[0]), (run, bad[:16])
