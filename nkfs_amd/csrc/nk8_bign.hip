@@ -486,6 +486,11 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_SLICE_BAR
 #define NKFS_BE_SLICE_BAR 0
 #endif
+// NKFS_BE_LATE_LOAD=1 (experiment builds): the next slice's loads after this
+// slice's stores; the progress count waits for the stores only
+#ifndef NKFS_BE_LATE_LOAD
+#define NKFS_BE_LATE_LOAD 0
+#endif
 constexpr int BE_WAVES = 16, BE_EW = 15;
 constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
 constexpr int BE_CMAX = 32;
@@ -699,7 +704,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     }
                 }
                 // the next slice's loads fly under this slice's stores
-                if (!last)
+                if (!NKFS_BE_LATE_LOAD && !last)
                     load(r0 + BE_ROWS);
                 // row quad -> one dword of 4 rows per part
                 if (r0 < v.ps) {
@@ -730,12 +735,26 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     // builtin alone does not: stores could sink below it),
                     // the asm wait for the hardware
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if constexpr (NKFS_BE_LATE_LOAD && KC != 0) {
+                        // the KC/4 loads of the next slice may stay in flight
+                        if (!last) {
+                            load(r0 + BE_ROWS);
+                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KC / 4) : "memory");
+                        } else {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        }
+                    } else {
+                        if (NKFS_BE_LATE_LOAD && !last)
+                            load(r0 + BE_ROWS);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
                     ++seq;
                     if (lane == 0)
                         __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (NKFS_BE_SLICE_BAR)
                         enc_barrier(&bar, gen, lane);
+                } else if (NKFS_BE_LATE_LOAD && !last) {
+                    load(r0 + BE_ROWS);
                 }
             }
         }
