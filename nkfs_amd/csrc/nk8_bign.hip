@@ -486,10 +486,12 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_SLICE_BAR
 #define NKFS_BE_SLICE_BAR 0
 #endif
-// NKFS_BE_LATE_LOAD=1 (experiment builds): the next slice's loads after this
-// slice's stores; the progress count waits for the stores only
+// NKFS_BE_LATE_LOAD (default 1): the next slice's loads issue after this
+// slice's stores, and the progress count waits for the stores only -- a
+// vmcnt(0) after the loads made every slice's signal wait for the next
+// slice's loads (W2 1,559 -> 1,690 GB/s, profiles/r05/ab_w2_late_load.txt)
 #ifndef NKFS_BE_LATE_LOAD
-#define NKFS_BE_LATE_LOAD 0
+#define NKFS_BE_LATE_LOAD 1
 #endif
 constexpr int BE_WAVES = 16, BE_EW = 15;
 constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
@@ -703,7 +705,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         }
                     }
                 }
-                // the next slice's loads fly under this slice's stores
+                // (NKFS_BE_LATE_LOAD 0: the next slice's loads before the stores)
                 if (!NKFS_BE_LATE_LOAD && !last)
                     load(r0 + BE_ROWS);
                 // row quad -> one dword of 4 rows per part
