@@ -110,6 +110,8 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
             return;
         }
         s = g.order ? g.order[p] : u32(p);
+        if (s >= g.nstripes)  // never an index past the batch (a torn order entry)
+            s = WSP_DEAD;
     };
     auto sched_geom = [&](u32 s, RingStripe &r) {
         r.s = s;
