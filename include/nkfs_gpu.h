@@ -62,13 +62,15 @@ int nkfs_gpu_get_devices(int *devices, int max);
  * to fill the chip); NKFS_ENC_WIDE_WS: part-group encoder with XXH64 fused
  * (a hash wave per workgroup; the default for k <= 16 batches that fill the
  * chip); NKFS_ENC_GENERIC: thread-per-row kernel; NKFS_ENC_BIG:
- * column-chunked encoder (any k; the default for k > 16) */
+ * column-chunked encoder (any k; the default for k > 32, and for 16 < k <= 32
+ * without digests -- with digests the stage-free encoder, tune enc_bign) */
 /* NKFS_ENC_WSP: persistent warp-specialised encoder (n <= 8, k <= 8, with
  * digests; ragged batches in size order from a device-wide group counter) */
 enum { NKFS_ENC_AUTO = 0, NKFS_ENC_WALK, NKFS_ENC_FUSED, NKFS_ENC_WS, NKFS_ENC_GENERIC, NKFS_ENC_WIDE, NKFS_ENC_BIG,
        NKFS_ENC_WIDE_WS, NKFS_ENC_WSP };
 /* NKFS_DEC_WIDE: survivor-table decoder (k <= 16; the default for 8 < k <= 16);
- * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16);
+ * NKFS_DEC_BIG: column-chunked decoder (any k; the default for k > 16 where
+ * the stage-free decoder does not apply, tune dec_bign);
  * NKFS_DEC_RUN: run decoder (k <= 8: persistent waves, each walking one
  * contiguous run of 1,024-row units across stripes) */
 /* NKFS_DEC_PAIR: k = 2 decoder (closed-form 2 x 2 inverse, one lookup per row) */
