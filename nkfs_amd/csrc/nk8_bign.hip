@@ -43,6 +43,7 @@
 #include "nk8_dev.h"
 #include "nkfs_internal.h"
 #include "runtime.h"
+#include "scratch.h"
 #include "xxh64_dev.h"
 
 using namespace nkfs;
@@ -493,6 +494,18 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_LATE_LOAD
 #define NKFS_BE_LATE_LOAD 1
 #endif
+// NKFS_BE_DYN=1 (experiment builds): units from per-XCD counters (a
+// workgroup takes the next unit of its own XCD -- a stripe's part groups stay
+// on one XCD -- and steals from the other XCDs' counters once its own runs
+// out, so every unit is taken even if an XCD holds no workgroup) instead of
+// the static walk b, b + grid, ...
+#ifndef NKFS_BE_DYN
+#define NKFS_BE_DYN 0
+#endif
+constexpr u32 BE_END = 0xFFFFFFFFu;
+
+// this wave's XCC (hardware register XCC_ID, bits 3:0)
+__device__ inline u32 be_xcc() { return u32(__builtin_amdgcn_s_getreg(20 | (3 << 11))) & 7u; }
 constexpr int BE_WAVES = 16, BE_EW = 15;
 constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
 constexpr int BE_CMAX = 32;
@@ -519,25 +532,62 @@ __device__ __forceinline__ u32 be_stripe(u32 u, u32 ngroups, u32 &grp)
 
 template <bool HASH, int KC>
 __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, const u8 *ids, u64 *digests,
-                                                                   u32 ngroups, u32 nunits)
+                                                                   u32 ngroups, u32 nunits, u32 *uctr)
 {
     __shared__ __attribute__((aligned(16))) u8 tbl[BE_CMAX * 4096];
     __shared__ u32 done[BE_WAVES];  // slices stored so far, per encoder wave
     __shared__ u32 bar;
+    __shared__ u32 uq[8];           // NKFS_BE_DYN: the workgroup's claimed units, in order
+    __shared__ u32 uq_n, hdone;     // claims published / units the hash wave finished
+    const bool dyn = NKFS_BE_DYN && uctr;
 
     const int n = g.n, k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nch = (k + 15) >> 4;
     if (tid < BE_WAVES)
         done[tid] = 0;
-    if (tid == 0)
+    if (tid == 0) {
         bar = 0;
+        uq_n = 0;
+        hdone = 0;
+    }
     __syncthreads();
 
     if (wave < BE_EW) {
         u32 gen = 0, seq = 0;
 #pragma unroll 1
-        for (u32 u = blockIdx.x; u < nunits; u += gridDim.x) {
+        for (u32 ci = 0;; ++ci) {
+            u32 u;
+            if (dyn) {
+                enc_barrier(&bar, gen, lane);  // the previous unit's lookups are done
+                if (wave == 0) {
+                    // at most 8 claims ahead of the hash wave (the uq ring)
+                    while (ci >= __hip_atomic_load(&hdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 8u)
+                        __builtin_amdgcn_s_sleep(8);
+                    u32 uu = BE_END;
+                    if (lane == 0) {
+                        const u32 x0 = be_xcc();
+                        for (u32 t = 0; t < 8; ++t) {
+                            const u32 xx = (x0 + t) & 7u;
+                            const u32 cand = atomicAdd(uctr + xx, 1u) * 8u + xx;
+                            if (cand < nunits) {
+                                uu = cand;
+                                break;
+                            }
+                        }
+                        uq[ci % 8] = uu;
+                        __hip_atomic_store(&uq_n, ci + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                enc_barrier(&bar, gen, lane);  // the claim is visible
+                u = uq[ci % 8];
+                if (u == BE_END)
+                    break;
+            } else {
+                u = blockIdx.x + ci * gridDim.x;
+                if (u >= nunits)
+                    break;
+            }
             u32 grp;
             const u32 s = be_stripe(u, ngroups, grp);
             if (s >= g.nstripes)
@@ -764,7 +814,21 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
         const int e = lane >> 2, a = lane & 3;
         u32 seq = 0;
 #pragma unroll 1
-        for (u32 u = blockIdx.x; u < nunits; u += gridDim.x) {
+        for (u32 ci = 0;; ++ci) {
+            u32 u;
+            if (dyn) {
+                if (lane == 0)
+                    __hip_atomic_store(&hdone, ci, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                while (__hip_atomic_load(&uq_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= ci)
+                    __builtin_amdgcn_s_sleep(8);
+                u = uq[ci % 8];
+                if (u == BE_END)
+                    break;
+            } else {
+                u = blockIdx.x + ci * gridDim.x;
+                if (u >= nunits)
+                    break;
+            }
             u32 grp;
             const u32 s = be_stripe(u, ngroups, grp);
             if (s >= g.nstripes)
@@ -905,9 +969,20 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // rows in k/4 contiguous 16-byte loads (k-specialised kernels)
     const bool kc = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->blocks) | g->block_pitch) & 3) == 0;
     const int kk = kc && (k == 20 || k == 24 || k == 28 || k == 32) ? k : 0;
+    // NKFS_BE_DYN: 8 zeroed per-XCD unit counters from the launch's scratch
+    // (none to be had: the static walk)
+    Scratch sc;
+    u32 *uctr = nullptr;
+    if (NKFS_BE_DYN && digests) {
+        uctr = static_cast<u32 *>(sc.take(g, 256, st));
+        if (uctr && hipMemsetAsync(uctr, 0, 32, st) != hipSuccess) {
+            (void)hipGetLastError();
+            uctr = nullptr;
+        }
+    }
     auto go = [&](auto hash, auto kcon) {
         hipLaunchKernelGGL((k_encode_bign<decltype(hash)::value, decltype(kcon)::value>), dim3(grid),
-                           dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits));
+                           dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
     };
     auto pick = [&](auto hash) {
         switch (kk) {
@@ -922,5 +997,7 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         pick(std::true_type{});
     else
         pick(std::false_type{});
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    const int rc = hipGetLastError() == hipSuccess ? 0 : -EIO;
+    const int e = sc.finish();
+    return rc ? rc : e;
 }
