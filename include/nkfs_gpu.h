@@ -261,25 +261,35 @@ int nkfs_pages_dsum_batch(const uint8_t *const *d_pages,
  * synchronous (returns when the outputs are in host memory) and cuts the
  * batch into sub-batches of about `chunk_bytes` of blocks (0 = 32 MiB) that
  * flow through three streams per device lane, so H2D, kernels and D2H of
- * consecutive sub-batches overlap.  Contiguous host buffers that the HIP
- * runtime does not know as pinned are registered for the call (reference
- * counted: concurrent calls may share a buffer); page lists are gathered
- * into / scattered from pinned staging.  Only defined outputs are written:
+ * consecutive sub-batches overlap.  Contiguous host buffers are DMA'd
+ * directly when they are pinned allocations (hipHostMalloc, torch
+ * pin_memory) or lie inside an nkfs_host_register range; any other buffer
+ * (pageable memory, memory registered with hipHostRegister outside this
+ * library, a range straddling a registration) is staged through pinned
+ * scratch by host copies, as page lists are gathered into / scattered
+ * from it.  Nothing is registered for a call.  Only defined outputs are written:
  * part bytes between a part's size and its pitch are unspecified, bytes
  * between stripes and the blocks of stripes that fail to decode
  * (-EINVAL: fewer than k distinct ids) keep the caller's contents.
- * A buffer that starts inside a range registered through
- * nkfs_host_register but runs past its end is refused with -EBUSY (its
- * owner could unpin the registered part mid-copy); a call that fails
+ * A call that fails
  * publishes no status, digests or decoded pages of the sub-batches it did
  * not finish.  The calling thread is left with the library's device
  * current. */
 
 /* Pin a host range for the library's DMA once (e.g. a server's page pool),
- * so per-call pinning becomes a reference bump.  -EEXIST when the runtime
- * already knows the range as pinned (nothing to do). */
+ * so calls on it DMA directly instead of staging.  The range must stay
+ * mapped until nkfs_host_unregister; a call in flight holds a reference, so
+ * an unregister never unpins under it.  -EEXIST when the runtime already
+ * knows the range as pinned (nothing to do), -EBUSY when it partly overlaps
+ * a registered range. */
 int nkfs_host_register(void *p, size_t bytes);
 int nkfs_host_unregister(void *p);
+/* Host-path state, for tests and leak checks: out[0] registered ranges,
+ * out[1] registry references held by calls in flight, out[2] host lane
+ * threads running, out[3] host copy threads running, out[4] per-call
+ * contexts (stream + scratch) handed out and not yet returned.  Fills
+ * min(n, 5) values; returns 5. */
+int nkfs_host_state(uint64_t *out, int n);
 
 /* Host-memory form of nkfs_nk8_encode: blocks, ids, parts and digests in
  * host memory. */

@@ -111,6 +111,7 @@ _SIGS = {
     "nkfs_pipeline_check": (C.c_int, [C.c_int, vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, vp,
                                       C.c_uint32, C.c_uint64, C.c_char_p, C.c_size_t]),
     "nkfs_host_lane_plan": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int]),
+    "nkfs_host_state": (C.c_int, [vp, C.c_int]),
     "nkfs_percall_service": (C.c_int, [C.c_int]),
 }
 

@@ -274,6 +274,15 @@ def decode_pages(parts, part_off, n_slots: int, ids, avail, navail: int, k: int,
                                        _ptr(st), _ptr(ex), _ptr(bm), chunk_bytes)
 
 
+def host_state() -> dict:
+    """nkfs_host_state: registered ranges, registry references held by calls
+    in flight, host lane threads and copy threads running, contexts handed
+    out (a host call that returned leaves the middle three at zero)."""
+    arr = (C.c_uint64 * 5)()
+    lib().nkfs_host_state(arr, 5)
+    return dict(zip(("registered", "call_refs", "lanes", "copy_threads", "contexts"), (int(v) for v in arr)))
+
+
 def set_devices(devices) -> int:
     """nkfs_gpu_set_devices: device lanes of the host-memory entry points."""
     arr = (C.c_int * max(1, len(devices)))(*devices)

@@ -308,9 +308,8 @@ static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile 
 		return -ENOSYS;
 	}
 	int err = 0;
-	if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
-	    (err = svc_launch_locked()))
-		goto out;
+	/* the request is complete in the box before its number is published and
+	 * before any (re)launch, so a wave never reads half-written arguments */
 	g_svc->args = *a;
 	/* a message of at most 1 KiB of stripes travels inline: the wave reads
 	 * it in the same round trip as the arguments */
@@ -330,19 +329,30 @@ static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile 
 	const double t0 = g_svc_trace ? mono_us() : 0;
 	double t1 = 0;
 	__atomic_store_n(&g_svc->seq, sq, __ATOMIC_RELEASE);
+	if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
+	    (err = svc_launch_locked()))
+		goto out;
 	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag; spin++) {
 		if (g_svc_trace && !t1 && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) == sq)
 			t1 = mono_us();
-		if ((spin & 0xFFF) == 0xFFF && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) != sq &&
-		    !__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE)) {
-			/* the wave left without taking the request: relaunch once it is gone */
+		if ((spin & 0xFFF) == 0xFFF) {
+			/* the service stream's own status, whether or not the wave took
+			 * the request (a wave that faults or stalls after
+			 * taking it must not spin the caller forever) */
 			hipError_t q = hipStreamQuery(g_svc_stream);
-			if (q == hipSuccess) {
-				if ((err = svc_launch_locked()))
-					goto out;
-			} else if (q != hipErrorNotReady) {
+			if (q != hipSuccess && q != hipErrorNotReady) {
 				err = -EIO;
 				goto out;
+			}
+			if (q == hipSuccess && __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag) {
+				/* the wave is gone: it left before taking the request
+				 * (relaunch), or took it and never finished (error) */
+				if (__atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) == sq) {
+					err = -EIO;
+					goto out;
+				}
+				if ((err = svc_launch_locked()))
+					goto out;
 			}
 		}
 		__builtin_ia32_pause();

@@ -228,6 +228,30 @@ __device__ inline void run_desc_load(const nkfs_geom &g, int n_slots, const u8 *
         d.B = g.block_sizes[s + vz];
         d.poff = g.part_off[s + vz];
         d.boff = g.block_off[s + vz];
+#ifdef NKFS_DEBUG_BOUNDS
+        // debug-bounds build: a stripe whose block stores or survivor loads
+        // would leave the caller's buffers (or whose plan names a slot past
+        // n_slots) is reported and skipped like a stripe with fewer than K
+        // distinct ids
+        {
+            const u64 pp = (u64(part_size_of(d.B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
+            bool bad = (g.blocks_bytes && d.boff + d.B > g.blocks_bytes) ||
+                       (g.parts_bytes && d.poff + u64(n_slots) * pp > g.parts_bytes) || (d.poff & 15) ||
+                       (g.block_size && d.B > g.block_size) || s >= g.nstripes;
+            if ((d.pw[0] & 0xFFu) != 0xFFu)
+                for (int cc = 0; cc < K; ++cc)
+                    bad |= ((d.pw[cc / 4] >> (8 * (cc % 4))) & 0xFFu) >= u32(n_slots);
+            if (bad) {
+                if ((threadIdx.x & 63) == 0)
+                    printf("nkfs bounds: k_decode_run stripe %u chunk %u: B %u block [%llu,+%u) of %llu, parts "
+                           "[%llu,+%llu) of %llu\n",
+                           s, ci, d.B, (unsigned long long)d.boff, d.B, (unsigned long long)g.blocks_bytes,
+                           (unsigned long long)d.poff, (unsigned long long)(u64(n_slots) * pp),
+                           (unsigned long long)g.parts_bytes);
+                d.pw[0] |= 0xFFu;
+            }
+        }
+#endif
     } else {
         d.B = g.block_size;
         d.poff = u64(s) * u64(n_slots) * g.part_pitch;

@@ -124,6 +124,26 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
             r.B = g.block_sizes[s];
             r.boff = g.block_off[s];
             r.poff = g.part_off[s];
+#ifdef NKFS_DEBUG_BOUNDS
+            // debug-bounds build: report and skip a stripe whose block reads
+            // (dword-rounded) or part stores would leave the caller's buffers
+            {
+                const u64 pp = (u64(part_size_of(r.B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
+                if ((g.blocks_bytes && r.boff + ((u64(r.B) + 3) & ~u64(3)) > g.blocks_bytes) ||
+                    (g.parts_bytes && r.poff + u64(n) * pp > g.parts_bytes) || (r.poff & 15) ||
+                    (g.block_size && r.B > g.block_size) || r.B == 0) {
+                    printf("nkfs bounds: k_encode_wsp stripe %u: B %u block [%llu,+%u) of %llu, parts [%llu,+%llu) "
+                           "of %llu\n",
+                           s, r.B, (unsigned long long)r.boff, r.B, (unsigned long long)g.blocks_bytes,
+                           (unsigned long long)r.poff, (unsigned long long)(u64(n) * pp),
+                           (unsigned long long)g.parts_bytes);
+                    r.s = WSP_DEAD;
+                    r.B = 0;
+                    r.boff = r.poff = 0;
+                    return;
+                }
+            }
+#endif
         } else {
             r.B = g.block_size;
             r.boff = u64(s) * g.block_pitch;

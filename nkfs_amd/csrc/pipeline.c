@@ -16,11 +16,16 @@
  * next and the D2H of a third overlap.  Page lists are gathered into /
  * scattered from pinned staging by the host (a page pointer is caller
  * memory the GPU never dereferences); contiguous caller buffers go straight
- * over DMA (pinned for the call when the runtime does not know them, with a
- * reference-counted registry so concurrent calls on the same buffer never
- * unpin under each other).  Only bytes the API defines as outputs are
- * written back: part runs of abutting stripes, blocks of stripes that
- * decoded (gaps and failed stripes keep the caller's bytes).
+ * over DMA only when they are pinned allocations (hipHostMalloc, torch
+ * pin_memory) or lie inside a range the caller registered once through
+ * nkfs_host_register; any other (pageable) buffer is staged through the
+ * context's pinned scratch by host copies, like a page list.  No DMA ever
+ * targets pageable memory the library did not pin by allocation: both
+ * host-path GPU faults of rounds 3 and 5 were DMA into pageable memory
+ * through the runtime's SVM mapping (tools/pin_probe.c).
+ * Only bytes the API defines as outputs are written back: part runs of
+ * abutting stripes, blocks of stripes that decoded (gaps and failed stripes
+ * keep the caller's bytes).
  *
  * With several device lanes (nkfs_gpu_set_devices) a batch is cut into
  * byte-balanced contiguous stripe ranges, one host thread and one device
@@ -49,13 +54,18 @@ struct pin_ent {
 	struct pin_ent *next;
 };
 static pthread_mutex_t g_pin_lock = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t g_pin_cv = PTHREAD_COND_INITIALIZER;
 static struct pin_ent *g_pins;
+static uint64_t g_pin_calls;   /* registry references held by in-flight calls */
+static int g_lanes_running;    /* host lane threads (atomics) */
+static int g_copy_threads;     /* host copy threads (atomics) */
 
-/* Does the runtime know [p, p+bytes) as pinned host memory in one piece?
- * The start pointer's attributes alone are not enough: a range that starts
- * inside a pinned allocation and runs past its end would be DMA'd partly
- * from pageable memory (round-3 fault audit). */
+/* Is [p, p+bytes) inside ONE pinned allocation of the runtime
+ * (hipHostMalloc, torch pin_memory)?  Only such memory is DMA'd without
+ * staging.  Memory registered with hipHostRegister outside this library
+ * reports no extent (hipMemGetAddressRange gives base NULL: it is a KFD SVM
+ * range over pageable pages, tools/pin_probe.c E4) and is staged: the
+ * library cannot know its lifetime, and DMA into pageable memory is what
+ * faulted. */
 static int runtime_pinned(const void *p, size_t bytes)
 {
 	hipPointerAttribute_t attr;
@@ -68,55 +78,26 @@ static int runtime_pinned(const void *p, size_t bytes)
 	const void *dp = attr.devicePointer ? attr.devicePointer : p;
 	if (hipMemGetAddressRange(&base, &size, (void *)dp) != hipSuccess || !base || !size) {
 		(void)hipGetLastError();
-		return 1; /* no extent known: the start pointer's word (caller contract) */
+		return 0;
 	}
 	/* the range's offset inside the allocation, in the allocation's own VA */
 	const uintptr_t off = (uintptr_t)dp - (uintptr_t)base;
 	return off + bytes >= off && off + bytes <= size;
 }
 
-/* Which of the registry's entries does [a, a+bytes) conflict with?  Returns
- * the entry it lies inside (NULL if none) and sets *busy_user / *busy_call
- * when it partly overlaps an entry registered by nkfs_host_register / by
- * another in-flight call.  Caller holds g_pin_lock. */
-static struct pin_ent *pin_find(uintptr_t a, size_t bytes, int *busy_user, int *busy_call)
+/* The registry holds only the caller's own registrations
+ * (nkfs_host_register).  Which entry is [a, a+bytes) inside (NULL if none)?
+ * *partial is set when it partly overlaps one.  Caller holds g_pin_lock. */
+static struct pin_ent *pin_find(uintptr_t a, size_t bytes, int *partial)
 {
-	*busy_user = *busy_call = 0;
+	*partial = 0;
 	for (struct pin_ent *e = g_pins; e; e = e->next) {
 		if (a >= e->base && a + bytes <= e->base + e->bytes)
 			return e;
-		if (a < e->base + e->bytes && e->base < a + bytes) {
-			if (e->urefs)
-				*busy_user = 1;
-			else
-				*busy_call = 1;
-		}
+		if (a < e->base + e->bytes && e->base < a + bytes)
+			*partial = 1;
 	}
 	return NULL;
-}
-
-/* Register [a, a+bytes) as a new entry (caller holds g_pin_lock). */
-static int pin_new(uintptr_t a, size_t bytes, int user, struct pin_ent **held)
-{
-	struct pin_ent *e = malloc(sizeof(*e));
-	if (!e)
-		return -ENOMEM;
-	hipError_t he = hipHostRegister((void *)a, bytes, hipHostRegisterPortable);
-	if (he != hipSuccess) {
-		(void)hipGetLastError();
-		free(e);
-		/* partly overlapping a registration made outside this registry:
-		 * refuse rather than DMA from memory that may be unpinned mid-copy */
-		return he == hipErrorHostMemoryAlreadyRegistered ? -EBUSY : nkfs_hip_fail("hipHostRegister", (int)he);
-	}
-	e->base = a;
-	e->bytes = bytes;
-	e->refs = 1;
-	e->urefs = user;
-	e->next = g_pins;
-	g_pins = e;
-	*held = e;
-	return 0;
 }
 
 /* caller holds g_pin_lock */
@@ -130,94 +111,54 @@ static void pin_drop_locked(struct pin_ent *e)
 			}
 		const hipError_t he = hipHostUnregister((void *)e->base);
 		if (he != hipSuccess) {
-			/* the runtime still holds it: say so (a later call on a reused
-			 * mapping would otherwise be trusted as pinned) */
 			(void)hipGetLastError();
 			nkfs_hip_fail("hipHostUnregister", (int)he);
 		}
 		free(e);
-		pthread_cond_broadcast(&g_pin_cv);
 	}
 }
 
-static void pin_drop(struct pin_ent *e)
-{
-	if (!e)
-		return;
-	pthread_mutex_lock(&g_pin_lock);
-	pin_drop_locked(e);
-	pthread_mutex_unlock(&g_pin_lock);
-}
-
-/* Pin the ranges a host call DMAs from / to ([p[i], p[i]+bytes[i]), i < 2;
- * NULL or empty ranges are skipped) for the duration of the call, in one
+/* How a host call reaches the ranges it copies from / to ([p[i],
+ * p[i]+bytes[i]), i < 2; NULL or empty ranges are skipped), decided in one
  * step under the registry lock:
- *  - memory the runtime already knows as pinned over the whole range
- *    (hipHostMalloc, torch pinned memory) needs nothing;
- *  - a range inside an entry of this registry takes a reference;
- *  - a range that partly overlaps an nkfs_host_register entry is refused
- *    (-EBUSY: the entry's owner could unpin it mid-copy);
- *  - a range that partly overlaps another call's temporary entry waits until
- *    that call drops it (nothing is held while waiting, so two calls cannot
- *    wait on each other);
- *  - anything else is registered here for the call.
- * Two ranges of one call that overlap each other are pinned as their union.
- * held[i] = the entry to release (NULL when nothing was taken). */
-static int pin_take2(const void *const p[2], const size_t bytes[2], struct pin_ent *held[2])
+ *  - inside an nkfs_host_register entry: a reference is taken (the owner's
+ *    unregister cannot unpin it mid-call) and the range is DMA'd directly;
+ *  - inside one pinned allocation of the runtime: DMA'd directly;
+ *  - anything else (pageable memory, a range straddling a registration):
+ *    staged through pinned scratch by host copies (direct[i] = 0).
+ * Nothing is registered for a call.  held[i] = the entry to release. */
+static void pin_take2(const void *const p[2], const size_t bytes[2], struct pin_ent *held[2], int direct[2])
 {
-	uintptr_t a[2] = { (uintptr_t)p[0], (uintptr_t)p[1] };
-	size_t nb[2] = { p[0] ? bytes[0] : 0, p[1] ? bytes[1] : 0 };
-	held[0] = held[1] = NULL;
-	int share = 0; /* range 1 rides on range 0's entry */
-	if (nb[0] && nb[1] && a[0] < a[1] + nb[1] && a[1] < a[0] + nb[0]) {
-		const uintptr_t lo = a[0] < a[1] ? a[0] : a[1];
-		const uintptr_t hi = a[0] + nb[0] > a[1] + nb[1] ? a[0] + nb[0] : a[1] + nb[1];
-		a[0] = lo;
-		nb[0] = hi - lo;
-		nb[1] = 0;
-		share = 1;
-	}
-	int rc = 0;
 	pthread_mutex_lock(&g_pin_lock);
-	/* the registry first (a range inside an in-flight call's entry must take
-	 * a reference: the runtime would also call it pinned, until that call
-	 * unpins it), then the runtime's own pinned allocations */
-	for (;;) {
-		int wait = 0;
-		for (int i = 0; i < 2 && !rc; i++) {
-			int bu, bc;
-			if (!nb[i] || pin_find(a[i], nb[i], &bu, &bc))
-				continue;
-			if (bu)
-				rc = -EBUSY;
-			else if (bc)
-				wait = 1;
-		}
-		if (rc || !wait)
-			break;
-		pthread_cond_wait(&g_pin_cv, &g_pin_lock);
-	}
-	for (int i = 0; i < 2 && !rc; i++) {
-		if (!nb[i])
+	for (int i = 0; i < 2; i++) {
+		held[i] = NULL;
+		direct[i] = 0;
+		if (!p[i] || !bytes[i])
 			continue;
-		int bu, bc;
-		struct pin_ent *in = pin_find(a[i], nb[i], &bu, &bc);
+		int partial;
+		struct pin_ent *in = pin_find((uintptr_t)p[i], bytes[i], &partial);
 		if (in) {
 			in->refs++;
 			held[i] = in;
-		} else if (!runtime_pinned((const void *)a[i], nb[i])) {
-			rc = pin_new(a[i], nb[i], 0, &held[i]);
+			direct[i] = 1;
+		} else {
+			direct[i] = runtime_pinned(p[i], bytes[i]);
 		}
 	}
-	if (rc)
-		for (int i = 0; i < 2; i++)
-			if (held[i]) {
-				pin_drop_locked(held[i]);
-				held[i] = NULL;
-			}
+	g_pin_calls += (held[0] != NULL) + (held[1] != NULL);
 	pthread_mutex_unlock(&g_pin_lock);
-	(void)share;
-	return rc;
+}
+
+static void pin_release2(struct pin_ent *held[2])
+{
+	pthread_mutex_lock(&g_pin_lock);
+	for (int i = 0; i < 2; i++)
+		if (held[i]) {
+			g_pin_calls--;
+			pin_drop_locked(held[i]);
+			held[i] = NULL;
+		}
+	pthread_mutex_unlock(&g_pin_lock);
 }
 
 int nkfs_host_register(void *p, size_t bytes)
@@ -227,17 +168,28 @@ int nkfs_host_register(void *p, size_t bytes)
 	const uintptr_t a = (uintptr_t)p;
 	int rc = 0;
 	pthread_mutex_lock(&g_pin_lock);
-	int bu, bc;
-	struct pin_ent *in = pin_find(a, bytes, &bu, &bc), *e = NULL;
+	int partial;
+	struct pin_ent *in = pin_find(a, bytes, &partial);
 	if (in) {
 		in->refs++;
 		in->urefs++; /* now also the caller's registration */
-	} else if (bu || bc) {
+	} else if (partial) {
 		rc = -EBUSY;
 	} else if (runtime_pinned(p, bytes)) {
 		rc = -EEXIST; /* pinned by its owner: nothing to hold */
 	} else {
-		rc = pin_new(a, bytes, 1, &e);
+		struct pin_ent *e = malloc(sizeof(*e));
+		hipError_t he = e ? hipHostRegister(p, bytes, hipHostRegisterPortable) : hipErrorOutOfMemory;
+		if (!e) {
+			rc = -ENOMEM;
+		} else if (he != hipSuccess) {
+			(void)hipGetLastError();
+			free(e);
+			rc = he == hipErrorHostMemoryAlreadyRegistered ? -EBUSY : nkfs_hip_fail("hipHostRegister", (int)he);
+		} else {
+			*e = (struct pin_ent){ a, bytes, 1, 1, g_pins };
+			g_pins = e;
+		}
 	}
 	pthread_mutex_unlock(&g_pin_lock);
 	return rc;
@@ -285,6 +237,8 @@ struct hp {
 	uint64_t *badmask;
 	int32_t *status;
 	uint64_t chunk;
+	/* pageable contiguous sides staged through pinned scratch (hp_run) */
+	int stage_blk, stage_parts;
 };
 
 static uint32_t hp_B(const struct hp *h, uint32_t s) { return h->sizes ? h->sizes[s] : h->block_size; }
@@ -321,7 +275,7 @@ static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
  * (offsets into the context buffers). */
 struct lay {
 	uint64_t d_blk, d_parts, d_boff, d_poff, d_sz, d_ids, d_avail, d_dig, d_status, d_bad, d_work, d_scr, d_total;
-	uint64_t h_boff, h_poff, h_sz, h_ids, h_avail, h_dig, h_status, h_bad, h_stage, h_total;
+	uint64_t h_boff, h_poff, h_sz, h_ids, h_avail, h_dig, h_status, h_bad, h_stage, h_pstage, h_total;
 };
 
 struct sub {
@@ -428,103 +382,156 @@ static void layout(const struct hp *h, uint32_t cnt, uint64_t blk_bytes, uint64_
 	o += align256(cnt * 4ull);
 	L->h_bad = o;
 	o += align256(cnt * 8ull);
-	L->h_stage = o;
-	o += hp_paged(h) ? align256(blk_bytes) : 0;
+	L->h_stage = o; /* blocks: gathered pages or a staged pageable range */
+	o += hp_paged(h) || h->stage_blk ? align256(blk_bytes) : 0;
+	L->h_pstage = o; /* parts: a staged pageable range */
+	o += h->stage_parts ? align256(part_bytes) : 0;
 	L->h_total = o;
 }
 
-/* copy block s of a page list into dst (gather) or back (scatter) */
-static void page_copy(const struct hp *h, uint32_t s, uint8_t *buf, int to_pages)
+/* ------------------------------------------------------------ host copies */
+
+/* Host copies between caller memory and pinned staging -- page gathers and
+ * scatters, staged pageable ranges -- go through one list of (dst, src,
+ * len) pieces run by a few threads: one memcpy stream tops out near 10
+ * GB/s, below what PCIe moves.  Pieces are at most CP_PIECE bytes so a
+ * single contiguous range spreads over the threads too. */
+#define COPY_THREADS 4
+#define CP_PIECE (1u << 20)
+
+struct cp {
+	uint8_t *dst;
+	const uint8_t *src;
+	size_t len;
+};
+
+struct cpl {
+	struct cp *v;
+	size_t n, cap;
+	uint64_t bytes;
+};
+
+static void cpl_add(struct cpl *l, uint8_t *dst, const uint8_t *src, size_t len)
 {
-	const uint32_t B = hp_B(h, s), P = h->page_size;
-	uint8_t *const *pg = h->pages + h->first_page[s];
-	for (uint32_t off = 0, i = 0; off < B; off += P, i++) {
-		const uint32_t len = B - off < P ? B - off : P;
-		if (to_pages)
-			memcpy(pg[i], buf + off, len);
-		else
-			memcpy(buf + off, pg[i], len);
+	while (len) {
+		const size_t piece = len < CP_PIECE ? len : CP_PIECE;
+		if (l->n == l->cap) {
+			const size_t cap = l->cap ? 2 * l->cap : 256;
+			struct cp *v = realloc(l->v, cap * sizeof(*v));
+			if (!v) { /* no list: copy now, on this thread */
+				memcpy(dst, src, len);
+				return;
+			}
+			l->v = v;
+			l->cap = cap;
+		}
+		l->v[l->n++] = (struct cp){ dst, src, piece };
+		l->bytes += piece;
+		dst += piece;
+		src += piece;
+		len -= piece;
 	}
+}
+
+struct cpj {
+	const struct cp *v;
+	size_t a, b;
+};
+
+static void *cpj_run(void *arg)
+{
+	const struct cpj *j = arg;
+	for (size_t i = j->a; i < j->b; i++)
+		memcpy(j->v[i].dst, j->v[i].src, j->v[i].len);
+	return NULL;
+}
+
+/* Run the list (byte-balanced contiguous shares, COPY_THREADS threads from
+ * 4 MiB on) and empty it; every thread is joined before this returns. */
+static void cpl_run(struct cpl *l)
+{
+	int nt = l->bytes >= (4u << 20) ? COPY_THREADS : 1;
+	if ((size_t)nt > l->n)
+		nt = (int)l->n;
+	if (nt < 1)
+		nt = 1;
+	struct cpj jb[COPY_THREADS];
+	pthread_t th[COPY_THREADS];
+	int started[COPY_THREADS] = { 0 };
+	uint64_t acc = 0;
+	size_t a = 0;
+	for (int t = 0; t < nt; t++) {
+		const uint64_t goal = l->bytes * (uint64_t)(t + 1) / (uint64_t)nt;
+		size_t b = a;
+		while (b < l->n && (t == nt - 1 || acc < goal || b == a))
+			acc += l->v[b++].len;
+		jb[t] = (struct cpj){ l->v, a, b };
+		a = b;
+	}
+	for (int t = 1; t < nt; t++) {
+		started[t] = pthread_create(&th[t], NULL, cpj_run, &jb[t]) == 0;
+		if (started[t])
+			__atomic_add_fetch(&g_copy_threads, 1, __ATOMIC_RELAXED);
+	}
+	cpj_run(&jb[0]);
+	for (int t = 1; t < nt; t++) {
+		if (started[t]) {
+			pthread_join(th[t], NULL);
+			__atomic_sub_fetch(&g_copy_threads, 1, __ATOMIC_RELAXED);
+		} else {
+			cpj_run(&jb[t]);
+		}
+	}
+	l->n = 0;
+	l->bytes = 0;
+}
+
+static void cpl_free(struct cpl *l)
+{
+	free(l->v);
+	memset(l, 0, sizeof(*l));
 }
 
 /* Gather (to_pages 0) or scatter (1) the blocks of stripes [s0, s1) between
  * their page lists and the packed staging `buf` (block s at its packed
- * 256-byte-aligned offset), stripes with skip[s - s0] set left alone.  A
- * few host threads share the stripes: one memcpy stream tops out near
- * 10 GB/s, below what PCIe moves. */
-#define COPY_THREADS 4
-
-struct pcopy {
-	const struct hp *h;
-	uint32_t s0, s1;
-	uint8_t *buf;
-	const uint64_t *off; /* packed offset of each stripe in [s0, s1) */
-	const int32_t *status;
-	int to_pages;
-};
-
-static void *pcopy_run(void *arg)
+ * 256-byte-aligned offset), stripes with status[s - s0] == -EINVAL left
+ * alone. */
+static int pages_copy(const struct hp *h, uint32_t s0, uint32_t s1, uint8_t *buf, uint64_t cap,
+		      const int32_t *status, int to_pages)
 {
-	const struct pcopy *c = arg;
-	for (uint32_t s = c->s0; s < c->s1; s++)
-		if (!c->status || c->status[s] != -EINVAL)
-			page_copy(c->h, s, c->buf + c->off[s], c->to_pages);
-	return NULL;
+	struct cpl l = { 0 };
+	uint64_t o = 0;
+	const uint32_t P = h->page_size;
+	for (uint32_t s = s0; s < s1; s++) {
+		const uint32_t B = hp_B(h, s);
+		if (o + B > cap || o + B < o) { /* the staging region (always checked) */
+			cpl_free(&l);
+			return -ERANGE;
+		}
+		if (!status || status[s - s0] != -EINVAL) {
+			uint8_t *const *pg = h->pages + h->first_page[s];
+			for (uint32_t off = 0, i = 0; off < B; off += P, i++) {
+				const uint32_t len = B - off < P ? B - off : P;
+				if (to_pages)
+					cpl_add(&l, pg[i], buf + o + off, len);
+				else
+					cpl_add(&l, buf + o + off, pg[i], len);
+			}
+		}
+		o += align256(B);
+	}
+	cpl_run(&l);
+	cpl_free(&l);
+	return 0;
 }
 
-static void pages_copy(const struct hp *h, uint32_t s0, uint32_t s1, uint8_t *buf, const int32_t *status,
-		       int to_pages)
+/* One contiguous range between caller memory and staging (threaded). */
+static void range_copy(uint8_t *dst, const uint8_t *src, uint64_t len)
 {
-	const uint32_t cnt = s1 - s0;
-	uint64_t *off = malloc((size_t)cnt * sizeof(*off));
-	if (!off) { /* no scratch: one thread, offsets on the fly */
-		uint64_t o = 0;
-		for (uint32_t s = s0; s < s1; s++) {
-			if (!status || status[s - s0] != -EINVAL)
-				page_copy(h, s, buf + o, to_pages);
-			o += align256(hp_B(h, s));
-		}
-		return;
-	}
-	uint64_t o = 0, total = 0;
-	for (uint32_t s = 0; s < cnt; s++) {
-		off[s] = o;
-		o += align256(hp_B(h, s0 + s));
-	}
-	total = o;
-	int nt = total >= (4u << 20) ? COPY_THREADS : 1;
-	if ((uint32_t)nt > cnt)
-		nt = (int)cnt;
-	struct pcopy pc[COPY_THREADS];
-	pthread_t th[COPY_THREADS];
-	int started[COPY_THREADS] = {0};
-	/* byte-balanced contiguous stripe ranges, indices relative to s0 */
-	uint32_t a = 0;
-	for (int i = 0; i < nt; i++) {
-		const uint64_t goal = total * (uint64_t)(i + 1) / (uint64_t)nt;
-		uint32_t b = a;
-		while (b < cnt && (i == nt - 1 || off[b] < goal || b == a))
-			b++;
-		pc[i] = (struct pcopy){ h, a, b, buf, off, status, to_pages };
-		a = b;
-	}
-	/* pcopy_run indexes stripes relative to s0: shift the page lists */
-	struct hp hs = *h;
-	hs.first_page = h->first_page + s0;
-	if (h->sizes)
-		hs.sizes = h->sizes + s0;
-	for (int i = 0; i < nt; i++)
-		pc[i].h = &hs;
-	for (int i = 1; i < nt; i++)
-		started[i] = pthread_create(&th[i], NULL, pcopy_run, &pc[i]) == 0;
-	pcopy_run(&pc[0]);
-	for (int i = 1; i < nt; i++) {
-		if (started[i])
-			pthread_join(th[i], NULL);
-		else
-			pcopy_run(&pc[i]);
-	}
-	free(off);
+	struct cpl l = { 0 };
+	cpl_add(&l, dst, src, len);
+	cpl_run(&l);
+	cpl_free(&l);
 }
 
 /* Sub-batch u's metadata into the pinned scratch `hb` (layout L): ids
@@ -620,20 +627,28 @@ static int issue(const struct hp *h, struct ctxs *x)
 	/* payload in */
 	if (h->dir == HP_ENC) {
 		if (paged) {
-			pages_copy(h, u->s0, u->s1, hb + L->h_stage, NULL, 0);
+			if ((rc = pages_copy(h, u->s0, u->s1, hb + L->h_stage, L->h_pstage - L->h_stage, NULL, 0)))
+				goto out;
 			uint64_t o = 0;
 			for (uint32_t s = u->s0; s < u->s1; s++)
 				o += align256(hp_B(h, s));
 			HIPGO(hipMemcpyAsync(d + L->d_blk, hb + L->h_stage, o, hipMemcpyHostToDevice, st),
 			      "H2D (gathered pages)");
 		} else {
-			HIPGO(hipMemcpyAsync(d + L->d_blk, h->blocks + u->blo, u->bhi - u->blo, hipMemcpyHostToDevice,
-					     st),
-			      "H2D (blocks)");
+			const uint8_t *src = h->blocks + u->blo;
+			if (h->stage_blk) { /* pageable: through pinned staging */
+				range_copy(hb + L->h_stage, src, u->bhi - u->blo);
+				src = hb + L->h_stage;
+			}
+			HIPGO(hipMemcpyAsync(d + L->d_blk, src, u->bhi - u->blo, hipMemcpyHostToDevice, st), "H2D (blocks)");
 		}
 	} else {
-		HIPGO(hipMemcpyAsync(d + L->d_parts, h->parts + u->plo, u->phi - u->plo, hipMemcpyHostToDevice, st),
-		      "H2D (parts)");
+		const uint8_t *src = h->parts + u->plo;
+		if (h->stage_parts) {
+			range_copy(hb + L->h_pstage, src, u->phi - u->plo);
+			src = hb + L->h_pstage;
+		}
+		HIPGO(hipMemcpyAsync(d + L->d_parts, src, u->phi - u->plo, hipMemcpyHostToDevice, st), "H2D (parts)");
 	}
 
 	/* kernels (bases shifted so that the caller-relative offsets land in
@@ -676,8 +691,8 @@ static int issue(const struct hp *h, struct ctxs *x)
 			uint32_t e = s + 1;
 			while (e < u->s1 && hp_pofs(h, e) == hi)
 				hi += hp_pspan(h, e++);
-			HIPGO(hipMemcpyAsync(h->parts + lo, d + L->d_parts + (lo - u->plo), hi - lo,
-					     hipMemcpyDeviceToHost, st),
+			uint8_t *dst = h->stage_parts ? hb + L->h_pstage + (lo - u->plo) : h->parts + lo;
+			HIPGO(hipMemcpyAsync(dst, d + L->d_parts + (lo - u->plo), hi - lo, hipMemcpyDeviceToHost, st),
 			      "D2H (parts)");
 			s = e;
 		}
@@ -737,8 +752,9 @@ static int copy_blocks(const struct hp *h, struct ctxs *x)
 			while (e < u->s1 && stv[e - u->s0] != -EINVAL)
 				e++;
 			const uint64_t lo = hp_bofs(h, s);
-			HIPGO(hipMemcpy2DAsync(h->blocks + lo, h->block_pitch, x->d + x->L.d_blk + (lo - u->blo),
-					       h->block_pitch, h->block_size, e - s, hipMemcpyDeviceToHost, st),
+			uint8_t *dst = h->stage_blk ? x->hb + x->L.h_stage + (lo - u->blo) : h->blocks + lo;
+			HIPGO(hipMemcpy2DAsync(dst, h->block_pitch, x->d + x->L.d_blk + (lo - u->blo), h->block_pitch,
+					       h->block_size, e - s, hipMemcpyDeviceToHost, st),
 			      "D2H (blocks, pitched)");
 			s = e;
 		} else {
@@ -746,8 +762,8 @@ static int copy_blocks(const struct hp *h, struct ctxs *x)
 			uint32_t e = s + 1;
 			while (e < u->s1 && stv[e - u->s0] != -EINVAL && hp_bofs(h, e) == hi)
 				hi += hp_B(h, e++);
-			HIPGO(hipMemcpyAsync(h->blocks + lo, x->d + x->L.d_blk + (lo - u->blo), hi - lo,
-					     hipMemcpyDeviceToHost, st),
+			uint8_t *dst = h->stage_blk ? x->hb + x->L.h_stage + (lo - u->blo) : h->blocks + lo;
+			HIPGO(hipMemcpyAsync(dst, x->d + x->L.d_blk + (lo - u->blo), hi - lo, hipMemcpyDeviceToHost, st),
 			      "D2H (blocks)");
 			s = e;
 		}
@@ -774,14 +790,36 @@ static int retire(const struct hp *h, struct ctxs *x, int publish)
 	if (h->dir == HP_ENC) {
 		if (h->digests)
 			memcpy(h->digests + (uint64_t)u->s0 * nsl, x->hb + x->L.h_dig, (size_t)cnt * nsl * 8);
+		if (h->stage_parts) { /* the part runs issue() copied into staging */
+			struct cpl l = { 0 };
+			for (uint32_t s = u->s0; s < u->s1;) {
+				uint64_t lo = hp_pofs(h, s), hi = lo + hp_pspan(h, s);
+				uint32_t e = s + 1;
+				while (e < u->s1 && hp_pofs(h, e) == hi)
+					hi += hp_pspan(h, e++);
+				cpl_add(&l, h->parts + lo, x->hb + x->L.h_pstage + (lo - u->plo), hi - lo);
+				s = e;
+			}
+			cpl_run(&l);
+			cpl_free(&l);
+		}
 	} else {
 		const int32_t *stv = (const int32_t *)(x->hb + x->L.h_status);
 		if (h->status)
 			memcpy(h->status + u->s0, stv, (size_t)cnt * 4);
 		if (h->badmask)
 			memcpy(h->badmask + u->s0, x->hb + x->L.h_bad, (size_t)cnt * 8);
-		if (hp_paged(h))
-			pages_copy(h, u->s0, u->s1, x->hb + x->L.h_stage, stv, 1);
+		if (hp_paged(h)) {
+			rc = pages_copy(h, u->s0, u->s1, x->hb + x->L.h_stage, x->L.h_pstage - x->L.h_stage, stv, 1);
+		} else if (h->stage_blk) { /* the blocks of the stripes that decoded */
+			struct cpl l = { 0 };
+			for (uint32_t s = u->s0; s < u->s1; s++)
+				if (stv[s - u->s0] != -EINVAL)
+					cpl_add(&l, h->blocks + hp_bofs(h, s), x->hb + x->L.h_stage + (hp_bofs(h, s) - u->blo),
+						hp_B(h, s));
+			cpl_run(&l);
+			cpl_free(&l);
+		}
 	}
 out:
 	x->u.live = 0;
@@ -882,7 +920,9 @@ out:
 static void *lane_main(void *arg)
 {
 	struct lane *l = arg;
+	__atomic_add_fetch(&g_lanes_running, 1, __ATOMIC_RELAXED);
 	l->rc = run_lane(l->h, l->dev, l->s0, l->s1);
+	__atomic_sub_fetch(&g_lanes_running, 1, __ATOMIC_RELAXED);
 	return NULL;
 }
 
@@ -910,7 +950,6 @@ static int hp_run(struct hp *h)
 {
 	if (!h->chunk)
 		h->chunk = 32ull << 20;
-	const int nsl = hp_slots(h);
 	uint64_t bend = 0, pend = 0, total = 0;
 	for (uint32_t s = 0; s < h->nstripes; s++) {
 		const uint64_t be = hp_bofs(h, s) + hp_B(h, s), pe = hp_pofs(h, s) + hp_pspan(h, s);
@@ -918,13 +957,14 @@ static int hp_run(struct hp *h)
 		pend = pe > pend ? pe : pend;
 		total += hp_B(h, s);
 	}
-	(void)nsl;
 	struct pin_ent *held[2];
+	int direct[2];
 	const void *rp[2] = { hp_paged(h) ? NULL : h->blocks, h->parts };
 	const size_t rb[2] = { bend, pend };
-	int rc = pin_take2(rp, rb, held);
-	if (rc)
-		return rc;
+	pin_take2(rp, rb, held, direct);
+	h->stage_blk = !hp_paged(h) && !direct[0];
+	h->stage_parts = !direct[1];
+	int rc = 0;
 	/* struct nkfs_tune.host_lanes host threads per device: each lane keeps
 	 * its own host_depth sub-batches in flight, so one host thread blocked
 	 * on a stream never leaves the link idle */
@@ -967,9 +1007,26 @@ static int hp_run(struct hp *h)
 			rc = L[i].rc;
 		nkfs_use_device(nkfs_gpu_device());
 	}
-	pin_drop(held[1]);
-	pin_drop(held[0]);
+	pin_release2(held);
 	return rc;
+}
+
+int nkfs_host_state(uint64_t *out, int n)
+{
+	uint64_t v[5] = { 0 };
+	pthread_mutex_lock(&g_pin_lock);
+	for (struct pin_ent *e = g_pins; e; e = e->next)
+		v[0]++;
+	v[1] = g_pin_calls;
+	pthread_mutex_unlock(&g_pin_lock);
+	v[2] = (uint64_t)__atomic_load_n(&g_lanes_running, __ATOMIC_RELAXED);
+	v[3] = (uint64_t)__atomic_load_n(&g_copy_threads, __ATOMIC_RELAXED);
+	v[4] = nkfs_ctx_outstanding();
+	if (!out || n < 0)
+		return -EINVAL;
+	for (int i = 0; i < n && i < 5; i++)
+		out[i] = v[i];
+	return 5;
 }
 
 /* ------------------------------------------------------------ plan check */
@@ -1018,7 +1075,9 @@ int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *b
 	struct hp h = { .dir = decode ? HP_DEC : HP_ENC, .n = n_slots, .k = k, .n_slots = decode ? n_slots : 0,
 			.navail = decode ? navail : 0, .nstripes = nstripes, .max_block = max_block_size,
 			.sizes = block_size, .boff = page_size ? NULL : block_off, .poff = part_off, .ids = ids,
-			.avail = avail, .chunk = chunk_bytes ? chunk_bytes : 32ull << 20 };
+			.avail = avail, .chunk = chunk_bytes ? chunk_bytes : 32ull << 20,
+			/* pageable caller buffers: both sides staged (the default) */
+			.stage_blk = page_size ? 0 : 1, .stage_parts = 1 };
 	if (page_size) { /* page lists: only the packed staging matters here */
 		h.pages = (uint8_t *const *)first; /* non-NULL marker, never dereferenced */
 		h.first_page = first;
@@ -1070,6 +1129,9 @@ int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *b
 		}
 		CHK(in_range(u.plo, u.phi - u.plo, 0, pend), "sub-batch %d: part copy range", subs);
 		CHK(u.phi - u.plo <= L.d_boff - L.d_parts, "sub-batch %d: parts exceed the device region", subs);
+		/* host staging: gathered pages / a staged block range, a staged part range */
+		CHK(dev_block_bytes(&h, &u) <= L.h_pstage - L.h_stage, "sub-batch %d: block staging", subs);
+		CHK(u.phi - u.plo <= L.h_total - L.h_pstage, "sub-batch %d: part staging", subs);
 		CHK(sub_scratch(&h, &u) <= L.d_total - L.d_scr, "sub-batch %d: launcher scratch", subs);
 		CHK((uint64_t)cnt * n_slots * 8 <= L.d_status - L.d_dig, "sub-batch %d: digest region", subs);
 		CHK(nkfs_decode_work_bytes(cnt, k) <= L.d_scr - L.d_work, "sub-batch %d: decode workspace", subs);

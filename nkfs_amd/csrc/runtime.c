@@ -359,6 +359,13 @@ void nkfs_ctx_trim(void)
 
 /* A per-call context (stream + scratch) on `dev`, from its idle pool or new;
  * leaves `dev` current for the calling thread. */
+static uint64_t g_ctx_out; /* contexts handed out (atomics; nkfs_host_state) */
+
+uint64_t nkfs_ctx_outstanding(void)
+{
+	return __atomic_load_n(&g_ctx_out, __ATOMIC_RELAXED);
+}
+
 struct nkfs_ctx *nkfs_ctx_get_on(int dev)
 {
 	struct nkfs_ctx *c = NULL;
@@ -380,10 +387,13 @@ struct nkfs_ctx *nkfs_ctx_get_on(int dev)
 		if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 			goto fail;
 	}
+	__atomic_add_fetch(&g_ctx_out, 1, __ATOMIC_RELAXED);
 	return c;
 fail:
-	if (c)
+	if (c) {
+		__atomic_add_fetch(&g_ctx_out, 1, __ATOMIC_RELAXED); /* nkfs_ctx_put takes it back */
 		nkfs_ctx_put(c);
+	}
 	return NULL;
 }
 
@@ -398,6 +408,7 @@ void nkfs_ctx_put(struct nkfs_ctx *c)
 {
 	if (!c)
 		return;
+	__atomic_sub_fetch(&g_ctx_out, 1, __ATOMIC_RELAXED);
 	if (!c->stream) {
 		free(c);
 		return;

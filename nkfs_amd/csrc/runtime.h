@@ -41,6 +41,7 @@ void nkfs_gpu_release(void);
 void nkfs_ctx_trim(void);
 int nkfs_bad_params(uint32_t block_size, int n, int k);
 int nkfs_hip_fail(const char *what, int err);
+uint64_t nkfs_ctx_outstanding(void); /* contexts taken and not yet put back */
 int nkfs_host_depth(void); /* struct nkfs_tune.host_depth: sub-batches in flight per lane */
 int nkfs_host_lanes(void); /* struct nkfs_tune.host_lanes: host lanes per device */
 

@@ -187,6 +187,11 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle
             const u64 op = mb->op;
             if (op != NKFS_SVC_XXH && op != NKFS_SVC_XXH_INL) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // a stop uses a request number too: mark it taken, so the next
+                // wave (which starts from `taken`) sees no request pending
+                // (off -> on left taken one behind seq)
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(&mb->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;  // stop
             }
             nkfs_xxh_args a = mb->args;

@@ -224,10 +224,16 @@ def test_debug_bounds_build_compiles():
     syms = {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
     assert syms == exported()
     # the range checks are really compiled in: their report format is in the device code
-    strings = subprocess.run(["strings", os.path.join(csrc, "..", "build", "debug", "nk8_walk_k5.o")],
-                             capture_output=True, text=True, check=True).stdout
-    obj = subprocess.run(["grep", "-c", "nkfs bounds"], input=strings, capture_output=True, text=True)
-    assert int(obj.stdout.strip() or 0) >= 1
+    for o in ("nk8_walk_k5.o", "nk8_wsp.o", "nk8_run.o"):  # round 6: wsp + run decoder checked too
+        strings = subprocess.run(["strings", os.path.join(csrc, "..", "build", "debug", o)],
+                                 capture_output=True, text=True, check=True).stdout
+        obj = subprocess.run(["grep", "-c", "nkfs bounds"], input=strings, capture_output=True, text=True)
+        assert int(obj.stdout.strip() or 0) >= 1, o
+    # and none in the product's objects (no shared objects)
+    for o in ("nk8_wsp.o", "nk8_run.o"):
+        strings = subprocess.run(["strings", os.path.join(csrc, "..", "build", o)],
+                                 capture_output=True, text=True, check=True).stdout
+        assert "nkfs bounds" not in strings, o
 
 
 def test_host_lane_plan_interleaves_devices():

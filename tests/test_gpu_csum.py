@@ -237,3 +237,27 @@ def test_percall_service(L, O):
         assert L.nkfs_percall_service(0) == 0
     data = rng.integers(0, 256, 777, dtype=np.uint8)
     assert crt.xxh64(data) == O.xxh64(data)
+
+
+def test_percall_service_off_on(L, O):
+    """switching the service off (a stop request uses a request
+    number) and on again must not leave the next wave seeing a phantom
+    request.  On, off, on -- each time with the wave just stopped -- then an
+    inline message (<= 1 KiB) and one over 1 KiB against the oracle; and a
+    request right after a stop that the old wave may still be leaving."""
+    from nkfs_amd import crt
+    rng = np.random.default_rng(32)
+    for cycle in range(4):
+        assert L.nkfs_percall_service(1) == 0
+        try:
+            for n in (33, 1000, 1024, 1025, 4096 + 7):
+                data = rng.integers(0, 256, n, dtype=np.uint8)
+                assert crt.xxh64(data, cycle) == O.xxh64(data, cycle), (cycle, n)
+        finally:
+            assert L.nkfs_percall_service(0) == 0
+    assert L.nkfs_percall_service(1) == 0
+    try:
+        data = rng.integers(0, 256, 700, dtype=np.uint8)
+        assert crt.xxh64(data) == O.xxh64(data)
+    finally:
+        assert L.nkfs_percall_service(0) == 0

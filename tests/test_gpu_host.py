@@ -34,7 +34,38 @@ def O():
 
 
 def dev(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    """numpy -> device through a pinned bounce (no DMA from pageable memory
+    in the tests either: DESIGN.md §5.6)."""
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().cuda()
+
+
+def host(t):
+    """device tensor -> numpy through a pinned buffer."""
+    out = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    out.copy_(t)
+    return out.numpy()
+
+
+def pinned_np(nbytes, fill=None):
+    """a pinned (hipHostMalloc) uint8 numpy array: DMA'd directly by the
+    host entry points, where pageable arrays are staged."""
+    a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+    if fill is not None:
+        a[:] = fill
+    return a
+
+
+@pytest.fixture(autouse=True)
+def host_state_clean(L):
+    """Every host call leaves nothing behind: no registry reference, lane or
+    copy thread, and the same registrations and contexts as before
+    (VERDICT r05 item 1)."""
+    from nkfs_amd import batch
+    before = batch.host_state()
+    yield
+    after = batch.host_state()
+    assert after["call_refs"] == 0 and after["lanes"] == 0 and after["copy_threads"] == 0, after
+    assert after["registered"] == before["registered"] and after["contexts"] == before["contexts"], (before, after)
 
 
 def u64(x):
@@ -105,7 +136,7 @@ def test_decode_host_round_trip(L, O, S, B, n, k, chunk, pitch_pad):
     parts, _ = batch.encode(blocks, B, n, k, dev(ids_np))
     torch.cuda.synchronize()
     pitch = batch.part_pitch(B, k)
-    pn = parts.cpu().numpy().reshape(S, n, pitch)
+    pn = host(parts).reshape(S, n, pitch)
     # survivors: k random slots per stripe, packed as the caller holds them
     pick = np.stack([rng.permutation(n)[:k] for _ in range(S)])
     held = np.ascontiguousarray(pn[np.arange(S)[:, None], pick])          # [S, k, pitch]
@@ -119,7 +150,7 @@ def test_decode_host_round_trip(L, O, S, B, n, k, chunk, pitch_pad):
     rc = batch.decode_host(held.reshape(-1), pitch, k, hid.reshape(-1), avail.reshape(-1), k, k, B, out, bp,
                            status=status, chunk_bytes=chunk)
     assert rc == 0
-    want = blocks.cpu().numpy()[:, :B]
+    want = host(blocks)[:, :B]
     got = out.reshape(S, bp)
     ok = np.ones(S, bool)
     ok[bad] = False
@@ -144,8 +175,8 @@ def test_decode_host_verify(L):
     parts, dig = batch.encode(blocks, B, n, k, dev(ids_np))
     torch.cuda.synchronize()
     pitch = batch.part_pitch(B, k)
-    pn = parts.cpu().numpy().copy().reshape(-1)
-    dg = dig.cpu().numpy()
+    pn = host(parts).copy().reshape(-1)
+    dg = host(dig)
     pn[(9 * n + 2) * pitch + 100] ^= 1
     avail = np.tile(np.array([2, 0, 4, 6, 7, 1], np.uint8), (S, 1))
     out = np.zeros(S * B, np.uint8)
@@ -156,35 +187,39 @@ def test_decode_host_verify(L):
     assert status[9] == -5 and badmask[9] == 1 << 2
     others = np.arange(S) != 9
     assert (status[others] == 0).all() and (badmask[others] == 0).all()
-    assert np.array_equal(out.reshape(S, B)[others], blocks.cpu().numpy()[others, :B])
+    assert np.array_equal(out.reshape(S, B)[others], host(blocks)[others, :B])
 
 
 # ---------------------------------------------------------------- ragged, gaps
 
+@pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("n,k,chunk", [(8, 5, 0), (4, 2, 1 << 20), (6, 3, 100000)])
-def test_ragged_host_gaps_untouched(L, n, k, chunk):
+def test_ragged_host_gaps_untouched(L, n, k, chunk, pinned):
     """PUT and GET of a ragged batch whose block and part ranges have gaps
     between stripes: parts/blocks equal the device-resident result and
-    every gap byte keeps the caller's sentinel (pipeline.c)."""
+    every gap byte keeps the caller's sentinel (ADVICE r1, pipeline.c);
+    pageable buffers (staged) and pinned ones (direct DMA) alike."""
     from nkfs_amd import batch
+    alloc = pinned_np if pinned else (lambda nb, fill: np.full(nb, fill, np.uint8))
     sizes = synth.mixed_sizes(29)
     sizes[:3] = (1048576, 1, 70001)
     boff, poff, pos, ppos = ragged_layout(sizes, n, k, block_gap=24, part_gap=48)
-    host = np.full(pos, SENT, np.uint8)
+    hostb = alloc(pos, SENT)
     for s, B in enumerate(sizes):
-        host[boff[s]: boff[s] + B] = synth.stripe_bytes(900 + s, int(B))
+        hostb[boff[s]: boff[s] + B] = synth.stripe_bytes(900 + s, int(B))
+    host_ = hostb
     ids_np = synth.batch_ids(len(sizes), n, first=900)
-    parts_h = np.full(ppos, SENT, np.uint8)
+    parts_h = alloc(ppos, SENT)
     dig_h = np.zeros(len(sizes) * n, np.int64)
-    batch.encode_ragged_host(host, boff, sizes.astype(np.int32), n, k, ids_np, parts_h, poff, dig_h,
+    batch.encode_ragged_host(host_, boff, sizes.astype(np.int32), n, k, ids_np, parts_h, poff, dig_h,
                              chunk_bytes=chunk)
     parts_d = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
     dig_d = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
-    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts_d, dev(poff),
+    batch.encode_ragged(dev(host_), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts_d, dev(poff),
                         dig_d, int(sizes.max()))
     torch.cuda.synchronize()
-    assert np.array_equal(dig_h, dig_d.cpu().numpy())
-    pd = parts_d.cpu().numpy()
+    assert np.array_equal(dig_h, host(dig_d))
+    pd = host(parts_d)
     inside = np.zeros(ppos, bool)
     for s, B in enumerate(sizes):
         pitch, ps = batch.part_pitch(int(B), k), batch.part_size(int(B), k)
@@ -196,7 +231,7 @@ def test_ragged_host_gaps_untouched(L, n, k, chunk):
     # GET from every slot back into a sentinel-filled buffer with gaps
     rng = np.random.default_rng(n)
     avail = np.stack([rng.permutation(n) for _ in sizes]).astype(np.uint8)
-    out = np.full(pos, SENT, np.uint8)
+    out = alloc(pos, SENT)
     status = np.full(len(sizes), 7, np.int32)
     assert batch.decode_ragged_host(parts_h, poff, n, ids_np, avail, n, k, out, boff, sizes.astype(np.int32),
                                     status=status, chunk_bytes=chunk) == 0
@@ -204,7 +239,7 @@ def test_ragged_host_gaps_untouched(L, n, k, chunk):
     blk = np.zeros(pos, bool)
     for s, B in enumerate(sizes):
         blk[boff[s]: boff[s] + B] = True
-    assert np.array_equal(out[blk], host[blk]) and (out[~blk] == SENT).all()
+    assert np.array_equal(out[blk], host_[blk]) and (out[~blk] == SENT).all()
 
 
 # ---------------------------------------------------------------- page lists
@@ -236,8 +271,8 @@ def test_pages_put_get(L, O, n, k, chunk, page):
     batch.encode_ragged(dev(packed), dev(boff), dev(sz32), n, k, dev(ids_np), parts_d, dev(poff), dig_d,
                         int(sizes.max()))
     torch.cuda.synchronize()
-    assert np.array_equal(dig_h, dig_d.cpu().numpy())
-    pd = parts_d.cpu().numpy()
+    assert np.array_equal(dig_h, host(dig_d))
+    pd = host(parts_d)
     for s, B in enumerate(sizes):
         pitch, ps = batch.part_pitch(int(B), k), batch.part_size(int(B), k)
         for i in range(n):
@@ -275,13 +310,13 @@ def test_lanes_split_identical(L):
     ndev = L.nkfs_gpu_count()
     lanes = [0, 0, 0] if ndev < 2 else list(range(min(ndev, 4)))
     S, B, n, k = 1000, 65536, 8, 5
-    host = np.ascontiguousarray(batch.synth(S, B, first=3).cpu().numpy())
+    host_ = np.ascontiguousarray(host(batch.synth(S, B, first=3)))
     ids_np = synth.batch_ids(S, n, first=3)
-    ref_parts, ref_dig = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=4 << 20)
+    ref_parts, ref_dig = batch.encode_host(host_, B, n, k, ids_np, chunk_bytes=4 << 20)
     try:
         assert batch.set_devices(lanes) == 0
         assert batch.get_devices() == lanes
-        parts, dig = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=4 << 20)
+        parts, dig = batch.encode_host(host_, B, n, k, ids_np, chunk_bytes=4 << 20)
         assert torch.equal(parts[:, :batch.part_size(B, k)], ref_parts[:, :batch.part_size(B, k)])
         assert torch.equal(dig, ref_dig)
         out = np.zeros(S * B, np.uint8)
@@ -289,7 +324,7 @@ def test_lanes_split_identical(L):
         avail = np.tile(np.array([7, 6, 5, 4, 3], np.uint8), (S, 1))
         assert batch.decode_host(parts.numpy().reshape(-1), batch.part_pitch(B, k), n, ids_np.reshape(-1),
                                  avail.reshape(-1), k, k, B, out, B, status=status, chunk_bytes=4 << 20) == 0
-        assert (status == 0).all() and np.array_equal(out.reshape(S, B), host[:, :B])
+        assert (status == 0).all() and np.array_equal(out.reshape(S, B), host_[:, :B])
         # ragged, byte-balanced over the lanes
         sizes = synth.mixed_sizes(300)
         boff, poff, pos, ppos = ragged_layout(sizes, n, k)
@@ -330,15 +365,15 @@ def test_concurrent_calls_share_pageable_buffer(L):
     memory another call is still copying (pipeline.c pin())."""
     from nkfs_amd import batch
     S, B, n, k = 600, 65536, 8, 5
-    host = np.ascontiguousarray(batch.synth(S, B, first=8).cpu().numpy())
+    host_ = np.ascontiguousarray(host(batch.synth(S, B, first=8)))
     ids_np = synth.batch_ids(S, n, first=8)
-    ref, ref_dig = batch.encode_host(host, B, n, k, ids_np)
+    ref, ref_dig = batch.encode_host(host_, B, n, k, ids_np)
     errs = []
 
     def work():
         try:
             for _ in range(3):
-                p, d = batch.encode_host(host, B, n, k, ids_np, chunk_bytes=2 << 20)
+                p, d = batch.encode_host(host_, B, n, k, ids_np, chunk_bytes=2 << 20)
                 assert torch.equal(d, ref_dig)
         except Exception as e:  # noqa: BLE001 - reported below
             errs.append(e)
@@ -363,12 +398,14 @@ def test_host_register_api(L):
     assert L.nkfs_host_register(pinned.data_ptr(), 4096) == -17  # -EEXIST: runtime-pinned
 
 
-def test_partial_overlap_with_registration_is_busy(L):
-    """A host call whose buffer starts inside a range this library pinned
-    (nkfs_host_register) but runs past its end is refused with -EBUSY before
-    any copy, instead of DMA-ing from memory the owner may unpin mid-copy
-    (pipeline.c pin_take); the range alone and the range inside
-    the registration both work."""
+def test_partial_overlap_with_registration_is_staged(L):
+    """A host call whose buffer starts inside a range registered through
+    nkfs_host_register but runs past its end is staged through pinned
+    scratch (no DMA touches it, so its owner may unregister at any time);
+    the range inside the registration is DMA'd directly and holds a
+    reference only while the call runs.  All three give the digests of an
+    unrelated copy of the same bytes (round 6: nothing is registered for a
+    call)."""
     from nkfs_amd import batch
     B, n, k = 65536, 8, 5
     buf = np.zeros(4 * B, np.uint8)
@@ -376,17 +413,81 @@ def test_partial_overlap_with_registration_is_busy(L):
     ids_np = synth.batch_ids(2, n, first=77)
     assert L.nkfs_host_register(buf.ctypes.data, 2 * B) == 0
     try:
-        inside = buf[: 2 * B].reshape(2, B)
-        p_in, d_in = batch.encode_host(inside, B, n, k, ids_np)
-        straddle = buf[B: 3 * B].reshape(2, B)
-        with pytest.raises(OSError) as ei:
-            batch.encode_host(straddle, B, n, k, ids_np)
-        assert ei.value.errno == 16  # EBUSY
+        assert batch.host_state()["registered"] >= 1
+        p_in, d_in = batch.encode_host(buf[: 2 * B].reshape(2, B), B, n, k, ids_np)
+        p_st, d_st = batch.encode_host(buf[B: 3 * B].reshape(2, B), B, n, k, ids_np)
+        assert batch.host_state()["call_refs"] == 0
     finally:
         assert L.nkfs_host_unregister(buf.ctypes.data) == 0
-    p_out, d_out = batch.encode_host(buf[B: 3 * B].reshape(2, B), B, n, k, ids_np)  # unregistered: fine
     p_ref, d_ref = batch.encode_host(np.ascontiguousarray(buf[B: 3 * B]).reshape(2, B), B, n, k, ids_np)
-    assert torch.equal(d_out, d_ref)
+    p_r0, d_r0 = batch.encode_host(np.ascontiguousarray(buf[: 2 * B]).reshape(2, B), B, n, k, ids_np)
+    assert torch.equal(d_st, d_ref) and torch.equal(d_in, d_r0)
+    ps = batch.part_size(B, k)
+    assert torch.equal(p_st[:, :ps], p_ref[:, :ps]) and torch.equal(p_in[:, :ps], p_r0[:, :ps])
+
+
+def test_registration_overlap_refused(L):
+    """nkfs_host_register of a range that partly overlaps a registered one
+    is -EBUSY; the same range again is a second reference."""
+    buf = np.zeros(1 << 18, np.uint8)
+    p = buf.ctypes.data
+    assert L.nkfs_host_register(p, 1 << 17) == 0
+    try:
+        assert L.nkfs_host_register(p + (1 << 16), 1 << 17) == -16
+    finally:
+        assert L.nkfs_host_unregister(p) == 0
+
+
+@pytest.mark.parametrize("n,k,chunk", [(6, 3, 200000), (8, 5, 1 << 20)])
+def test_staged_equals_direct(L, n, k, chunk):
+    """The round-5 fault geometry (N6K3, 200,000-B sub-batches, mixed sizes
+    with 1 MiB, 1 B and page-edge stripes) through every buffer kind: PUT and
+    GET from pageable arrays (staged), pinned arrays (direct DMA) and a
+    registered range give identical parts, digests and blocks."""
+    from nkfs_amd import batch
+    sizes = synth.mixed_sizes(26)
+    sizes[:4] = (1048576, 1, 512, 513)
+    boff, poff, pos, ppos = ragged_layout(sizes, n, k, block_gap=8, part_gap=16)
+    src = np.full(pos, SENT, np.uint8)
+    for s, B in enumerate(sizes):
+        src[boff[s]: boff[s] + B] = synth.stripe_bytes(3000 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=3000)
+    sz32 = sizes.astype(np.int32)
+    rng = np.random.default_rng(n)
+    avail = np.stack([rng.permutation(n)[:k] for _ in sizes]).astype(np.uint8)
+    results = []
+    for kind in ("pageable", "pinned", "registered"):
+        if kind == "pinned":
+            bl, pa, out = pinned_np(pos, SENT), pinned_np(ppos, SENT), pinned_np(pos, SENT)
+        else:
+            bl, pa, out = np.full(pos, SENT, np.uint8), np.full(ppos, SENT, np.uint8), np.full(pos, SENT, np.uint8)
+        bl[:] = src
+        regs = []
+        if kind == "registered":
+            for a in (bl, pa, out):
+                assert L.nkfs_host_register(a.ctypes.data, a.nbytes) == 0
+                regs.append(a.ctypes.data)
+        try:
+            dg = np.zeros(len(sizes) * n, np.int64)
+            batch.encode_ragged_host(bl, boff, sz32, n, k, ids_np, pa, poff, dg, chunk_bytes=chunk)
+            st = np.full(len(sizes), 9, np.int32)
+            assert batch.decode_ragged_host(pa, poff, n, ids_np, avail, k, k, out, boff, sz32, status=st,
+                                            chunk_bytes=chunk) == 0
+            assert (st == 0).all()
+            assert batch.host_state()["call_refs"] == 0
+        finally:
+            for p in regs:
+                assert L.nkfs_host_unregister(p) == 0
+        assert np.array_equal(out, src), kind
+        results.append((pa.copy(), dg.copy()))
+    defined = np.zeros(ppos, bool)  # part bytes (the pitch padding is unspecified)
+    for s, B in enumerate(sizes):
+        pitch, ps = batch.part_pitch(int(B), k), batch.part_size(int(B), k)
+        for i in range(n):
+            defined[poff[s] + i * pitch: poff[s] + i * pitch + ps] = True
+    for pa, dg in results[1:]:
+        assert np.array_equal(dg, results[0][1])
+        assert np.array_equal(pa[defined], results[0][0][defined])
 
 
 # ---------------------------------------------------------------- general path, big parts
@@ -404,8 +505,8 @@ def test_generic_parts_beyond_grid_y(L, O):
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     mul = O.gf_mul_table()
-    blk = blocks[0, :B].cpu().numpy()
-    pn = parts.cpu().numpy()
+    blk = host(blocks[0, :B])
+    pn = host(parts)
     for j in (0, 65535 * 256 + 3, ps - 1):
         row = np.zeros(k, np.uint8)
         seg = blk[j * k: j * k + k]
@@ -431,7 +532,7 @@ def test_synth_ragged_matches_uniform(L):
     buf = torch.full((pos,), SENT, dtype=torch.uint8, device="cuda")
     batch.synth_ragged(buf, dev(boff), dev(sizes.astype(np.int32)), first=40)
     torch.cuda.synchronize()
-    got = buf.cpu().numpy()
+    got = host(buf)
     inside = np.zeros(pos, bool)
     for s, B in enumerate(sizes):
         assert np.array_equal(got[boff[s]: boff[s] + B], synth.stripe_bytes(40 + s, int(B))), s
