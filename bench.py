@@ -1,7 +1,7 @@
 """bench.py -- device-resident N-K encode(+XXH64 of every part)+decode
 throughput on MI355X, one process per GPU, stripes partitioned over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config all|c2|c3|c4|c5|w1|w2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config all|c2|c3|c4|c5|w1|w2|w3]
                     [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
@@ -17,8 +17,8 @@ value = user bytes of the whole job x K steps / max-over-ranks wall time.
 The same line carries the other configs as sub-objects under "configs"
 (c3s8: the 1,024-stripe per-GPU shard of the strong N=8 run, timed on one
 GPU; C2: 65,536 x 4 KiB N4K2; C4: 16,384 x 256 KiB N8K5; C5: the ragged
-4 KiB / 64 KiB / 1 MiB mix, byte-balanced over the ranks; W1/W2: the general
-n, k paths), each timed over at least 200 ms with its own roofline.
+4 KiB / 64 KiB / 1 MiB mix, byte-balanced over the ranks; W1/W2/W3: the general
+n, k paths, W3 with k = 41 > 32), each timed over at least 200 ms with its own roofline.
 
 The dominant kernel's roofline is measured live with HIP events on the
 stream the library launches on (torch's current stream); algorithmic bytes
@@ -60,6 +60,10 @@ CONFIGS = {
     # crt/nk8.c:735-744): the column-chunked kernels (nk8_big.hip), XXH64 a second pass over the parts
     "w2": (256, 1048576, 48, 32, "W2: N=48,K=32 encode(+XXH64/part)+decode(16 erased), 256 x 1 MiB stripes per "
                                  "GPU (k > 16 path; not a BASELINE config)"),
+    # k > 32 with rows of an odd byte count (most of the reference's k domain, its self
+    # test's k uniform in [2, 254], lies above 32)
+    "w3": (256, 1048576, 64, 41, "W3: N=64,K=41 encode(+XXH64/part)+decode(23 erased), 256 x 1 MiB stripes per "
+                                 "GPU (k > 32, odd k path; not a BASELINE config)"),
     # ragged: block size of every stripe drawn from C5_SIZES (synth.mixed_sizes)
     "c5": (11520, None, 8, 5, "C5: N=8,K=5 encode(+XXH64/part)+decode(3 erased) of a ragged batch, stripe sizes "
                               "uniform over {4 KiB, 64 KiB, 1 MiB}, ~4 GiB per GPU, byte-balanced over the GPUs"),
@@ -328,6 +332,7 @@ def box_stream(src, dst, read_bytes, write_bytes, stream):
 
 
 _ANCHOR = {}
+_BOX = {}
 
 
 def hbm_anchor(src, dst, stream):
@@ -367,6 +372,24 @@ def hbm_anchor(src, dst, stream):
     out["kernel"] = "boxprobe.hip k_copy4/k_read4/k_write4: grid-stride float4, 256 threads/WG"
     _ANCHOR.update(out)
     return _ANCHOR
+
+
+def box_clock(stream):
+    """CU count, the runtime's peak shader clock and the clock a busy grid
+    runs at on this box (boxprobe.hip k_clock: s_memtime cycles against the
+    100 MHz s_memrealtime) -- VERDICT r05 item 4: box-to-box swings of the
+    same kernels are attributed with it."""
+    import ctypes as C
+    P = probe_lib()
+    if P is None or not hasattr(P, "nkfs_probe_clock"):
+        return None
+    P.nkfs_probe_clock.restype = C.c_int
+    P.nkfs_probe_clock.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    mhz, cus, peak = C.c_double(0), C.c_int(0), C.c_int(0)
+    if P.nkfs_probe_clock(stream.cuda_stream, C.byref(mhz), C.byref(cus), C.byref(peak)) != 0:
+        return None
+    return {"cus": cus.value, "sclk_peak_mhz": peak.value, "sclk_loaded_mhz": round(mhz.value, 1),
+            "probe": "boxprobe.hip k_clock: 4 waves per CU, dependent integer chain, s_memtime vs s_memrealtime"}
 
 
 def anchor_mix(read_bytes, write_bytes):
@@ -524,6 +547,8 @@ def run_uniform(name, args, rank, world, device, steps, stripes=0, strong_total=
     # the box's own ceiling for each kernel's read:write mix, on the
     # kernel's own buffers (after verification: the probe overwrites them)
     hbm_anchor(blocks, parts, stream)
+    if not _BOX:
+        _BOX.update(box_clock(stream) or {})
     box_enc = box_stream(blocks, parts, S * B, S * n * ps, stream)
     box_dec = box_stream(parts, out, S * k * ps, S * B, stream)
     res = uniform_result(name, args, rank, world, device, S, B, n, k, desc, strong_total, steps, elapsed, enc_s,
@@ -686,6 +711,8 @@ def compose_line(args, rank, world, top, subs):
         result["verified"] = bool(result["verified"]) and all(v["verified"] for v in subs.values())
     if _ANCHOR:
         result["hbm_anchor"] = dict(_ANCHOR)
+    if _BOX:
+        result["box"] = dict(_BOX)
     if rank == 0 and not args.no_cpu:
         result["cpu_model"] = cpu_model()
     if getattr(args, "tune", ""):
@@ -739,7 +766,7 @@ def main():
             # the per-GPU shard of the headline's strong N=8 run, timed on one
             # GPU now (kernel choice and per-GPU efficiency at 1,024 stripes)
             subs["c3s8"] = run("c3", None, CONFIGS["c3"][0] // 8)
-        for name in ("c2", "c4", "c5", "w1", "w2"):
+        for name in ("c2", "c4", "c5", "w1", "w2", "w3"):
             subs[name] = run(name, None)
     result = compose_line(args, rank, world, top, subs)
     if rank == 0:

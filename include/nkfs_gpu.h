@@ -105,14 +105,17 @@ struct nkfs_tune {
 	int enc_persist;      /* n > 4 with digests: the persistent warp-specialised encoder (NKFS_ENC_WSP) where the
 	                         automatic choice is the walk encoder (ragged batches: 1, the default) or also the
 	                         warp-specialised grid (uniform batches: 2); 0 = off */
-	int dec_bign;         /* k > 8 decode on the stage-free decoder (nk8_bign.hip): -2 = auto (byte tables for
-	                         k > 16 and k % 4 == 0 below 16), -1 = off (survivor-table / column-chunked
+	int dec_bign;         /* k > 8 decode on the stage-free decoder (nk8_bign.hip): -2 = auto (NKFS_DEC_AUTO only:
+	                         byte tables for k % 4 == 0 except 16, layout 3 for the other 16 < k <= 64),
+	                         -1 = off (survivor-table / column-chunked
 	                         decoders), 0 = byte tables, 1 = nibble tables x 16 replicas (every
 	                         lookup in its lane's own bank slot) in 16-survivor chunks, 2 = the same in 8-survivor
-	                         chunks (two workgroups per CU) */
-	int enc_bign;         /* k <= 32 encode on the stage-free encoder with a hash wave (nk8_bign.hip): -1 = auto
+	                         chunks (two workgroups per CU), 3 = every output column of a slice in one workgroup
+                         (8 < k <= 64; rows through an LDS stage, so odd k store whole 16-byte pieces) */
+	int enc_bign;         /* k <= 76 encode on the stage-free encoder with a hash wave (nk8_bign.hip; units of 16
+	                         parts up to k = 32, of 8 parts above): -1 = auto
 	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64
-	                         pass), 1 = every k <= 32 batch it accepts, persistent (a workgroup per CU walking
+	                         pass), 1 = every k <= 76 batch it accepts, persistent (a workgroup per CU walking
 	                         the (stripe, part group) units), 2 = the same, one workgroup per unit */
 	int dec_pair_pipe;    /* k = 2 decode of uniform batches of blocks <= 4 KiB (C2): waves per CU of the persistent
 	                         pipelined pair decoder (next stripes' slots, ids and parts in flight under the current

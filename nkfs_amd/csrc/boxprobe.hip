@@ -183,7 +183,51 @@ int run(const void *in, size_t in_bytes, void *out, size_t out_bytes, int waves_
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Shader clock under load: every wave spins a dependent integer chain and
+// reads the shader cycle counter (s_memtime) and the 100 MHz real-time
+// counter (s_memrealtime) around it (record the box's
+// clock in the line, to attribute box-to-box swings).
+__global__ __launch_bounds__(64) void k_clock(u64 *out, u32 iters)
+{
+    const u64 t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    u32 x = threadIdx.x + blockIdx.x;
+    for (u32 i = 0; i < iters; ++i)
+        x = x * 1664525u + 1013904223u;
+    const u64 t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r1 - r0;
+    }
+    if (x == 0x12345678u)
+        out[2] = x;  // keeps the chain
+}
+
 }  // namespace
+
+// Loaded shader clock (MHz) from k_clock over 4 waves per CU, and the CU
+// count and peak clock the runtime reports.
+extern "C" int nkfs_probe_clock(hipStream_t st, double *mhz_loaded, int *cus, int *mhz_peak)
+{
+    if (!mhz_loaded || !cus || !mhz_peak)
+        return -EINVAL;
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev) ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, dev))
+        return -ENODEV;
+    *mhz_peak = khz / 1000;
+    u64 *d = nullptr, h[3] = {0, 0, 0};
+    if (hipMalloc(reinterpret_cast<void **>(&d), 3 * sizeof(u64)) != hipSuccess)
+        return -ENOMEM;
+    hipLaunchKernelGGL(k_clock, dim3(4 * *cus), dim3(64), 0, st, d, 1u << 20);  // warm-up: clocks ramp
+    hipLaunchKernelGGL(k_clock, dim3(4 * *cus), dim3(64), 0, st, d, 1u << 22);
+    const bool ok = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok || !h[1])
+        return -EIO;
+    *mhz_loaded = double(h[0]) / (double(h[1]) / 100.0);  // s_memrealtime ticks at 100 MHz
+    return 0;
+}
 
 // Median time (ms) of `reps` launches streaming the read:write mix
 // read_kib:write_kib (one of 4:8, 5:8, 6:8, 8:8, 8:4) from `in` to `out` at

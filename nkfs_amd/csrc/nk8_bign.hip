@@ -454,6 +454,289 @@ int launch_bign(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// ---- decode, 8 < k <= 64: every output column of a slice in one workgroup
+// (struct nkfs_tune.dec_bign 3).  k_decode_bign gives
+// each 16-column output group its own workgroup, so a row's k bytes come
+// from ceil(k/16) workgroups and rows that are not dword multiples (odd k)
+// are written bytewise, 16-byte windows at a k-byte lane stride.  Here one
+// workgroup owns all NG = ceil(k/16) groups of its rows:
+//  - the stripe's K x K inverse (rows padded to 16 NG columns) and survivor
+//    slots are copied to LDS once per workgroup;
+//  - per slice of ROWS rows and per 16-survivor chunk, the chunk's survivor
+//    dwords are loaded once (the next chunk's in flight) and feed all NG
+//    groups: for each group the chunk's 16 byte tables U_c[x] = (W[c][16h]
+//    x, ..., W[c][16h+15] x) are built (64 KiB) and every lane folds its 4
+//    rows into the group's accumulators (acc[h], 16 bytes of 4 rows);
+//  - output: a lane's 4 rows are 4k contiguous block bytes.  Row q is
+//    shifted to its byte offset q k (a 64-bit funnel shift per dword, the
+//    shift uniform) and written to an LDS stage as dwords -- the dword a row
+//    shares with the next is OR-ed in (ds_or), the bytes past column k being
+//    zero -- then the wave reads the stage back as 16-byte pieces in lane
+//    order and stores them: every store instruction writes 1 KiB of
+//    contiguous block bytes, whatever k.  The stage reuses the table LDS, in
+//    two halves of the wave.
+// Survivors past k sit in a chunk's tail and are skipped (uniform); output
+// columns past k have zero W entries, so their accumulator bytes are zero.
+#ifndef BR_PAIRS
+#define BR_PAIRS 1  // survivor pairs whose lookups fly together in k_decode_bigr
+#endif
+template <int NG, int T>
+struct BrShape {
+    static constexpr int WAVES = 8, CW = 16, NT = 64 * WAVES;
+    static constexpr u32 ROWS = u32(NT) * 4u * u32(T);
+    static constexpr int KMAX = 16 * NG;
+    static constexpr u32 WL = u32(KMAX) * u32(KMAX);  // inverse rows x padded columns, bytes
+};
+
+#ifndef BR_PREFETCH
+// k_decode_bigr: 1 = the next chunk's survivor loads in flight under this
+// chunk's groups; 0 (default) = each chunk's loads at its start, covered by
+// the other workgroup on the CU (W3 875 vs 864, N40K17 1,700 vs 1,666 GB/s,
+// profiles/r06/ab_bigr_variants.txt)
+#define BR_PREFETCH 0
+#endif
+#ifndef BR_WPE
+#define BR_WPE 4
+#endif
+template <int NG, int T, bool PAL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_WPE))) void k_decode_bigr(nkfs_geom g, const u8 *work, const int32_t *status,
+                                                         u32 nslices, u32 nwg)
+{
+    using SH = BrShape<NG, T>;
+    constexpr int CW = SH::CW, NT = SH::NT, KP = SH::KMAX;
+    __shared__ __attribute__((aligned(16))) u8 tbl[CW * 4096];  // tables; the output stage after the lookups
+    __shared__ __attribute__((aligned(16))) u8 wl[SH::WL];      // wl[c * KP + m] = W[c][m], 0 for m >= k
+    __shared__ u32 wsoff[KP];                                   // survivor c's part offset (slot * pitch)
+
+    const u32 b = blockIdx.x;
+    const u32 s = b / nwg, wi = b % nwg;
+    if (s >= g.nstripes || (status && status[s]))
+        return;  // the whole workgroup
+    const Stripe v = stripe_at(g, s);  // g.blocks = the output, g.n = slots per stripe
+    if (wi * SH::ROWS >= v.ps)
+        return;
+    const int k = g.k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const u8 *wk = work + u64(s) * u64(k + k * k);
+    for (int i = tid; i < KP * KP; i += NT) {
+        const int c = i / KP, m = i % KP;
+        wl[i] = c < k && m < k ? wk[k + c * k + m] : u8(0);
+    }
+    if (tid < KP)
+        wsoff[tid] = tid < k ? u32(u64(wk[tid]) * v.pitch) : 0u;  // the launcher checks n * pitch < 2^32
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u8 *>(v.parts), (short)0, int(u64(g.n) * v.pitch), 0x00020000);
+    // survivor loads: slot offsets from LDS at each chunk's load (PAL: one
+    // buffer resource over the stripe's slots, the launcher checks n * pitch
+    // < 2^31; otherwise clamped byte loads)
+    auto load = [&](u32 (&d)[CW], u32 r4, int cc) {
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            if (CW * cc + j >= k)
+                break;  // uniform: survivors past k are never looked up
+            const u32 so = __builtin_amdgcn_readfirstlane(wsoff[CW * cc + j]);
+            if constexpr (PAL)
+                d[j] = __builtin_amdgcn_raw_buffer_load_b32(prs, so + r4, 0, 0);
+            else
+                d[j] = r4 < v.ps ? load4_any(v.parts + so + r4, v.ps - r4) : 0u;
+        }
+    };
+    // one row quad: the chunk's survivors' products for group h into a4
+    auto quad = [&](const u32 (&d)[CW], uint4 (&a4)[4], int cc) {
+        // tdep: 0 at run time, from an opaque move and then from the last
+        // pair's accumulator; folded into every survivor dword before its
+        // byte is extracted, so neither the extraction nor the address is
+        // shared between the NG groups of a chunk (common-subexpression
+        // elimination kept all 64 addresses of a chunk live across its groups:
+        // 205 VGPRs, one workgroup per CU), and a pair's lookups wait for the
+        // previous pair's (BR_PAIRS pairs in flight)
+        u32 tdep;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(tdep));
+#pragma unroll
+        for (int j = 0; j < CW; j += 2) {
+            if (CW * cc + j >= k)
+                break;  // uniform: survivors past k
+            // (odd k: the pair's second table is never built -- it may hold
+            // the previous slice's stage -- so it is not read)
+            const bool two = CW * cc + j + 1 < k;
+            const u32 dj0 = d[j] ^ tdep, dj1 = d[j + 1] ^ tdep;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32 sel = 0x0C0C0C00u | u32(4 + q);
+                const u32 P0 = __builtin_amdgcn_perm(dj0, 0u, sel) << 4;
+                const u32 P1 = __builtin_amdgcn_perm(dj1, 0u, sel) << 4;
+                const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
+                const uint4 c2 = two ? *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1)
+                                     : make_uint4(0, 0, 0, 0);
+                a4[q].x = xor3(a4[q].x, a.x, c2.x);
+                a4[q].y = xor3(a4[q].y, a.y, c2.y);
+                a4[q].z = xor3(a4[q].z, a.z, c2.z);
+                a4[q].w = xor3(a4[q].w, a.w, c2.w);
+            }
+            // one pair's 8 lookups in flight at a time (two pairs, as in
+            // k_decode_bign, cost this kernel 2 waves per SIMD: its NG
+            // accumulators and the next chunk's survivors are live too)
+            if ((j & (BR_PAIRS * 2 - 2)) == BR_PAIRS * 2 - 2)
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
+        }
+    };
+    // the 16 byte tables of chunk cc, group h (survivor j: W[16cc + j][16h ..])
+    auto build = [&](int cc, int h) {
+#pragma unroll 1
+        for (int j = wave; j < CW; j += SH::WAVES) {
+            const int c = CW * cc + j;
+            if (c >= k)
+                break;  // uniform
+            const uint4 r4 = *reinterpret_cast<const uint4 *>(wl + c * KP + 16 * h);
+            const u32 row[4] = {r4.x, r4.y, r4.z, r4.w};
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            build_table16(tbl + u32(j) * 4096u, basis, lane);
+        }
+    };
+
+    u8 *out = const_cast<u8 *>(v.blk);
+    const bool oal = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    // per row q of a lane's quad: the dword offset of its first byte in the
+    // lane's 4k-byte region and its byte shift (uniform)
+    u32 qd[4], qs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        qd[q] = (u32(q) * u32(k)) >> 2;
+        qs[q] = (u32(q) * u32(k)) & 3u;
+    }
+
+    for (u32 slice = wi; slice < nslices; slice += nwg) {
+        const u32 r_begin = slice * SH::ROWS;
+        if (r_begin >= v.ps)
+            break;
+        uint4 acc[T][NG][4];
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int h = 0; h < NG; ++h)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[t][h][q] = make_uint4(0, 0, 0, 0);
+        // survivor dwords, double-buffered over the chunks: chunk cc + 1's
+        // loads fly under chunk cc's NG table builds and lookups
+        u32 d[2][T][CW];
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            load(d[0][t], r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u, 0);
+#pragma unroll
+        for (int cc = 0; cc < NG; ++cc) {
+            if (!BR_PREFETCH && cc > 0)
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    load(d[cc & 1][t], r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u, cc);
+            if (BR_PREFETCH && cc + 1 < NG)
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    load(d[(cc + 1) & 1][t], r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u, cc + 1);
+#pragma unroll
+            for (int h = 0; h < NG; ++h) {
+                lds_barrier();  // the previous tables' lookups (or stage reads) are done
+                build(cc, h);
+                lds_barrier();
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    quad(d[cc & 1][t], acc[t][h], cc);
+            }
+        }
+        lds_barrier();  // every lookup is done: the table LDS becomes the stage
+
+        // ---- output through the stage, half a wave's lanes at a time
+        u8 *stage = tbl + u32(wave) * (32u * 4u * u32(KP));  // 32 lanes x 4 rows x KP bytes <= 8 KiB per wave
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const u32 wrow = r_begin + (u32(t) * u32(NT) + u32(wave) * 64u) * 4u;  // the wave's first row
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                if ((lane >> 5) == half) {
+                    const u32 base = u32(lane & 31) * u32(k);  // the lane's region, in dwords
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        u32 R[4 * NG];
+#pragma unroll
+                        for (int h = 0; h < NG; ++h) {
+                            R[4 * h] = acc[t][h][q].x;
+                            R[4 * h + 1] = acc[t][h][q].y;
+                            R[4 * h + 2] = acc[t][h][q].z;
+                            R[4 * h + 3] = acc[t][h][q].w;
+                        }
+                        const u32 sh = 32u - 8u * qs[q];  // 32: no shift
+                        const u32 nd = (qs[q] + u32(k) + 3u) >> 2;  // dwords the row touches
+#pragma unroll
+                        for (int w = 0; w <= 4 * NG; ++w) {
+                            if (u32(w) >= nd)
+                                break;  // uniform
+                            const u64 pair = (u64(w < 4 * NG ? R[w] : 0u) << 32) | (w ? R[w - 1] : 0u);
+                            const u32 dw = u32(pair >> sh);
+                            u32 *dst = reinterpret_cast<u32 *>(stage) + base + qd[q] + u32(w);
+                            if (w == 0 && qs[q])
+                                __hip_atomic_fetch_or(dst, dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                            else
+                                *dst = dw;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // the half's 32 x 4k bytes back in lane order, 16 bytes per lane
+                const u32 hbytes = 128u * u32(k);
+                const u64 obase = (u64(wrow) + u64(half) * 128u) * u64(k);  // block offset of the half's region
+#pragma unroll 1
+                for (u32 o = u32(lane) * 16u; o < hbytes; o += 1024u) {
+                    const u64 ob = obase + o;
+                    if (ob >= u64(v.B))
+                        break;
+                    const uint4 x = *reinterpret_cast<const uint4 *>(stage + o);
+                    if (oal && ob + 16u <= u64(v.B)) {
+                        store16(out + ob, x.x, x.y, x.z, x.w, false);
+                    } else {
+                        const u32 tw[4] = {x.x, x.y, x.z, x.w};
+                        for (u32 c = 0; c < 16u && ob + c < u64(v.B); ++c)
+                            out[ob + c] = u8(tw[c >> 2] >> (8 * (c & 3)));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // the stage is read before the next half overwrites it
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    }
+}
+
+template <int NG, int T>
+int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, bool pal, hipStream_t st)
+{
+    using SH = BrShape<NG, T>;
+    const int k = g->k;
+    const u32 ps_max = g->block_size / u32(k) + ((g->block_size % u32(k)) ? 1u : 0u);
+    const u64 nslices = (u64(ps_max) + SH::ROWS - 1) / SH::ROWS;
+    const u32 ns = u32(nslices ? nslices : 1);
+    // workgroups per stripe: enough for ~2 per CU in all, each walking its
+    // share of the stripe's slices (the inverse copied to LDS once)
+    const u64 want = (u64(nkfs_cu_count()) * 4 + u64(g->nstripes) - 1) / u64(g->nstripes);
+    const u32 nwg = u32(want < ns ? (want ? want : 1) : ns);
+    const u64 grid = u64(g->nstripes) * nwg;
+    if (grid > 0x7FFFFFFFull)
+        return -EINVAL;
+    // survivor offsets are 32-bit (a stripe's slots span < 4 GiB)
+    const u64 pitch_max = g->block_sizes ? (u64(ps_max) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1) : g->part_pitch;
+    if (u64(g->n) * pitch_max >= 0xFFFFFFFFull)
+        return -ENOSYS;
+    if (pal)
+        hipLaunchKernelGGL((k_decode_bigr<NG, T, true>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
+    else
+        hipLaunchKernelGGL((k_decode_bigr<NG, T, false>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 // ---- encode, k <= 32 ------------------------------------------------------
 // Reference arithmetic: crt/nk8.c:403-420 -- part_i[j] = XOR_m x_i^m
 // d[j*k+m], d zero past block_size (:393-398); XXH64 of every part
@@ -509,6 +792,14 @@ __device__ inline u32 be_xcc() { return u32(__builtin_amdgcn_s_getreg(20 | (3 <<
 constexpr int BE_WAVES = 16, BE_EW = 15;
 constexpr u32 BE_ROWS = 64u * BE_EW * 4u;  // 3,840 rows (120 XXH64 rounds) per slice
 constexpr int BE_CMAX = 32;
+// units of P = 8 parts (round 6, 32 < k <= 76): 8-byte table entries, k x 2
+// KiB of tables, so every column's table of a unit still stays resident
+constexpr int BE_CMAX8 = 76;
+template <int P>
+struct BeShape {
+    static constexpr u32 TB = 256u * u32(P);              // bytes per column table
+    static constexpr int CMAX = P == 16 ? BE_CMAX : BE_CMAX8;
+};
 
 // barrier of the encoder waves only (LDS counter; the hash wave runs on)
 __device__ __forceinline__ void enc_barrier(u32 *bar, u32 &gen, int lane)
@@ -530,11 +821,14 @@ __device__ __forceinline__ u32 be_stripe(u32 u, u32 ngroups, u32 &grp)
     return (loc / ngroups) * 8 + (u & 7);
 }
 
-template <bool HASH, int KC>
+template <int P, bool HASH, int KC>
 __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, const u8 *ids, u64 *digests,
                                                                    u32 ngroups, u32 nunits, u32 *uctr)
 {
-    __shared__ __attribute__((aligned(16))) u8 tbl[BE_CMAX * 4096];
+    static_assert(P == 16 || (P == 8 && KC == 0), "part groups of 16, or of 8 without contiguous-row loads");
+    constexpr u32 TB = BeShape<P>::TB;
+    constexpr int TPW = 64 / P;  // tables whose Vandermonde row one wave computes per pass
+    __shared__ __attribute__((aligned(16))) u8 tbl[BeShape<P>::CMAX * TB];
     __shared__ u32 done[BE_WAVES];  // slices stored so far, per encoder wave
     __shared__ u32 bar;
     __shared__ u32 uq[8];           // NKFS_BE_DYN: the workgroup's claimed units, in order
@@ -593,7 +887,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             if (s >= g.nstripes)
                 continue;  // the whole workgroup
             const Stripe v = stripe_at(g, s);
-            const int p0 = int(grp) * 16, np = min(16, n - p0);
+            const int p0 = int(grp) * P, np = min(P, n - p0);
 
             // every encoder wave is done with the previous unit's tables
             enc_barrier(&bar, gen, lane);
@@ -602,15 +896,17 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             // multiplication): lane 16t + e computes byte e of the wave's
             // table t (columns wave, wave + 15, wave + 30), the rows are
             // gathered into scalars; parts past n and columns past k: 0
+            // (P = 8: lane 8t + e, byte e of table t, t < 8: columns up to
+            // wave + 105 >= 76)
             u32 xb;
             {
-                const int t = lane >> 4, e = lane & 15, m = wave + BE_EW * t;
+                const int t = lane / P, e = lane % P, m = wave + BE_EW * t;
                 u32 r = 0;
-                if (e < np && m < k && t < 3) {
+                if (e < np && m < k && (P == 8 || t < 3)) {
                     u32 x = ids[u64(s) * u64(n) + u64(p0 + e)];
                     r = 1;
 #pragma unroll
-                    for (int bit = 0; bit < 5; ++bit) {
+                    for (int bit = 0; bit < 7; ++bit) {
                         if ((m >> bit) & 1)
                             r = gf_mul_packed(r, x);
                         x = gf_mul_packed(x, x);
@@ -619,31 +915,39 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 xb = r;
             }
 #pragma unroll 1
-            for (int t = 0; t < 3; ++t) {
+            for (int t = 0; t < (P == 16 ? 3 : TPW); ++t) {
                 const int m = wave + BE_EW * t;
-                if (m >= 16 * nch)
+                // P = 16: columns k .. 16 nch - 1 get zero tables (lookups in
+                // column pairs); P = 8: only columns < k exist -- 16 nch
+                // tables would overrun the LDS at k = 76 -- and a pair's
+                // second lookup past k is skipped instead
+                if (m >= (P == 16 ? 16 * nch : k))
                     break;  // uniform
                 if (m < k) {
-                    u32 row[4];
+                    u32 row[P / 4];
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) {
+                    for (int w = 0; w < P / 4; ++w) {
                         u32 r = 0;
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            r |= u32(__builtin_amdgcn_readlane(int(xb), 16 * t + 4 * w + i)) << (8 * i);
+                            r |= u32(__builtin_amdgcn_readlane(int(xb), P * t + 4 * w + i)) << (8 * i);
                         row[w] = r;
                     }
-                    u32 basis[8][4];
-                    make_basis<4>(basis, row);
-                    build_table16(tbl + m * 4096, basis, lane);
+                    u32 basis[8][P / 4];
+                    make_basis<P / 4>(basis, row);
+                    if constexpr (P == 16)
+                        build_table16(tbl + m * TB, basis, lane);
+                    else
+                        build_table<2, 64>(tbl + m * TB, basis, lane);
                 } else {  // columns k .. 16 nch - 1: zero (lookups go in column pairs)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        *reinterpret_cast<uint4 *>(tbl + m * 4096 + (lane + 64 * i) * 16) = make_uint4(0, 0, 0, 0);
+                    for (int i = 0; i < int(TB / 1024u); ++i)
+                        *reinterpret_cast<uint4 *>(tbl + m * TB + (lane + 64 * i) * 16) = make_uint4(0, 0, 0, 0);
                 }
             }
             enc_barrier(&bar, gen, lane);
 
+            if constexpr (P == 16) {
             // the block through a buffer resource based at the dword below
             // it: loads are dword aligned and anything past B reads 0 (the
             // bytes past B inside its last dword are masked in the last slice)
@@ -809,6 +1113,131 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     load(r0 + BE_ROWS);
                 }
             }
+            } else {
+            // P = 8 parts per unit, any k <= 76 (k > 32
+            // without the column-chunked encoder's second XXH64 pass): per
+            // slice, the lane's 4 rows in 16-column chunks -- a 16 + 4-byte
+            // load per row and chunk, aligned by v_alignbyte (the byte shift
+            // is uniform: a row starts at (4 l + q) k) -- chunk c + 1's loads
+            // in flight under chunk c's lookups; one ds_read_b64 gives a
+            // (row, column) term for the unit's 8 parts
+            const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<u8 *>(v.blk - mis), (short)0, int((v.B + mis + 3u) & ~3u), 0x00020000);
+            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 rl = u32(wave * 64 + lane) * 4u;
+            constexpr int NCH = (BE_CMAX8 + 15) / 16;
+            u32 raw[2][4][5];
+            auto load = [&](u32 (&x)[4][5], u32 r0, int c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32 a = ((r0 + u32(q)) * u32(k) + 16u * u32(c) + mis) & ~3u;
+                    const v4u y = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+                    x[q][0] = y.x;
+                    x[q][1] = y.y;
+                    x[q][2] = y.z;
+                    x[q][3] = y.w;
+                    x[q][4] = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
+                }
+            };
+            load(raw[0], rl, 0);
+#pragma unroll 1
+            for (u32 sl = 0; sl < nsl; ++sl) {
+                const u32 r0 = sl * BE_ROWS + rl;
+                const bool last = sl + 1 == nsl;
+                uint2 acc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = make_uint2(0, 0);
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    if (c >= nch)
+                        break;  // uniform
+                    if (c + 1 < nch)
+                        load(raw[(c + 1) & 1], r0, c + 1);
+                    u32 d[4][4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const u32 pos = (r0 + u32(q)) * u32(k) + 16u * u32(c);
+                        const u32 sh = (pos + mis) & 3u;
+#pragma unroll
+                        for (int w = 0; w < 4; ++w)
+                            d[q][w] = __builtin_amdgcn_alignbyte(raw[c & 1][q][w + 1], raw[c & 1][q][w], sh);
+                        if (last) {  // bytes at or past B are zero (crt/nk8.c:393-398)
+                            const u32 valid = v.B > pos ? min(v.B - pos, 16u) : 0u;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w) {
+                                const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
+                                d[q][w] &= u32((u64(1) << (8 * keep)) - 1u);
+                            }
+                        }
+                    }
+                    // columns in pairs, the bytes past k meet zero tables
+                    u32 tdep = 0;
+#pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        if (16 * c + j >= k)
+                            break;  // uniform
+                        const bool two = 16 * c + j + 1 < k;  // column j + 1 exists (no table past k)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
+                            const u32 s1 = 0x0C0C0C00u | u32(4 + ((j + 1) & 3));
+                            const u32 P0 = (__builtin_amdgcn_perm(d[q][j >> 2], 0u, s0) << 3) + tdep;
+                            const u32 P1 = (__builtin_amdgcn_perm(d[q][(j + 1) >> 2], 0u, s1) << 3) + tdep;
+                            const uint2 a = *reinterpret_cast<const uint2 *>(tbl + u32(16 * c + j) * TB + P0);
+                            const uint2 c2 = two ? *reinterpret_cast<const uint2 *>(tbl + u32(16 * c + j + 1) * TB + P1)
+                                                 : make_uint2(0, 0);
+                            acc[q].x = xor3(acc[q].x, a.x, c2.x);
+                            acc[q].y = xor3(acc[q].y, a.y, c2.y);
+                        }
+                        if (j & 2) {
+                            u32 z;
+                            asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(acc[3].x));
+                            tdep = z;
+                        }
+                    }
+                }
+                // row quad -> one dword of 4 rows per part
+                if (r0 < v.ps) {
+#pragma unroll
+                    for (int w = 0; w < 2; ++w) {
+                        const u32 *aw0 = &acc[0].x, *aw1 = &acc[1].x, *aw2 = &acc[2].x, *aw3 = &acc[3].x;
+                        u32 o[4];
+                        transpose4(aw0[w], aw1[w], aw2[w], aw3[w], o[0], o[1], o[2], o[3]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int e = 4 * w + i;
+                            if (e >= np)
+                                break;
+                            u8 *dst = v.parts + u64(p0 + e) * v.pitch + r0;
+                            if (r0 + 4u <= v.ps) {
+                                *reinterpret_cast<u32 *>(dst) = o[i];
+                            } else {
+                                for (u32 cb = 0; cb < 4 && r0 + cb < v.ps; ++cb)
+                                    dst[cb] = u8(o[i] >> (8 * cb));
+                            }
+                        }
+                    }
+                }
+                // the next slice's first chunk after the stores; the progress
+                // count waits for the stores only (the 8 loads stay in flight)
+                if constexpr (HASH) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (!last) {
+                        load(raw[0], r0 + BE_ROWS, 0);
+                        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    } else {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    ++seq;
+                    if (lane == 0)
+                        __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else if (!last) {
+                    load(raw[0], r0 + BE_ROWS, 0);
+                }
+            }
+            }
         }
     } else if constexpr (HASH) {
         const int e = lane >> 2, a = lane & 3;
@@ -834,7 +1263,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             if (s >= g.nstripes)
                 continue;
             const Stripe v = stripe_at(g, s);
-            const int p0 = int(grp) * 16, np = min(16, n - p0);
+            const int p0 = int(grp) * P, np = min(P, n - p0);  // P = 8: lanes 32.. idle (their e >= np)
             const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
             const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
             // the group's parts through one buffer resource (the launcher
@@ -921,7 +1350,7 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
                                 hipStream_t st)
 {
     const int k = g->k;
-    if (k < 2 || k > 254 || mode < 0 || mode > 2)
+    if (k < 2 || k > 254 || mode < 0 || mode > 3 || (mode == 3 && (k <= 8 || k > 64)))
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
@@ -934,7 +1363,14 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
     switch (mode) {
     case 0: return launch_bign<0>(g, work, status, pal, st);
     case 1: return launch_bign<1>(g, work, status, pal, st);
-    default: return launch_bign<2>(g, work, status, pal, st);
+    case 2: return launch_bign<2>(g, work, status, pal, st);
+    default:
+        switch ((k + 15) / 16) {
+        case 1: return launch_bigr<1, 1>(g, work, status, pal, st);
+        case 2: return launch_bigr<2, 1>(g, work, status, pal, st);
+        case 3: return launch_bigr<3, 1>(g, work, status, pal, st);
+        default: return launch_bigr<4, 1>(g, work, status, pal, st);
+        }
     }
 }
 
@@ -946,8 +1382,11 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
                                 hipStream_t st)
 {
     const int k = g->k, n = g->n;
-    if (k < 2 || k > BE_CMAX || n < k || g->part_min || g->part_max)
+    if (k < 2 || k > BE_CMAX8 || n < k || g->part_min || g->part_max)
         return -ENOSYS;
+    // k <= 32: units of 16 parts (16-byte table entries); 32 < k <= 76:
+    // units of 8 parts, whose k tables of 8-byte entries still fit the LDS
+    const int P = k <= BE_CMAX ? 16 : 8;
     if (!g->nstripes)
         return 0;
     // 4-byte aligned parts and pitch (dword stores); block offsets (rows +
@@ -957,7 +1396,7 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     if (((reinterpret_cast<uintptr_t>(g->parts) | (g->block_sizes ? 0 : g->part_pitch)) & 3) ||
         (ps_max + BE_ROWS) * u64(k) + 64 > 0x7FFFFFFFull || u64(n) * pitch_max > 0x7FFFFFFFull)
         return -ENOSYS;
-    const u64 ngroups = (u64(n) + 15) / 16;
+    const u64 ngroups = (u64(n) + u64(P) - 1) / u64(P);
     const u64 nunits = (u64(g->nstripes) + 7) / 8 * 8 * ngroups;
     if (nunits > 0x7FFFFFFFull)
         return -EINVAL;
@@ -968,7 +1407,7 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     // k % 4 == 0 with dword-aligned blocks (uniform batches): a lane's 4
     // rows in k/4 contiguous 16-byte loads (k-specialised kernels)
     const bool kc = !g->block_sizes && ((reinterpret_cast<uintptr_t>(g->blocks) | g->block_pitch) & 3) == 0;
-    const int kk = kc && (k == 20 || k == 24 || k == 28 || k == 32) ? k : 0;
+    const int kk = P == 16 && kc && (k == 20 || k == 24 || k == 28 || k == 32) ? k : 0;
     // NKFS_BE_DYN: 8 zeroed per-XCD unit counters from the launch's scratch
     // (none to be had: the static walk)
     Scratch sc;
@@ -981,10 +1420,15 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         }
     }
     auto go = [&](auto hash, auto kcon) {
-        hipLaunchKernelGGL((k_encode_bign<decltype(hash)::value, decltype(kcon)::value>), dim3(grid),
+        hipLaunchKernelGGL((k_encode_bign<16, decltype(hash)::value, decltype(kcon)::value>), dim3(grid),
                            dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
     };
     auto pick = [&](auto hash) {
+        if (P == 8) {
+            hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
+                               *g, ids, digests, u32(ngroups), u32(nunits), uctr);
+            return;
+        }
         switch (kk) {
         case 20: go(hash, std::integral_constant<int, 20>{}); break;
         case 24: go(hash, std::integral_constant<int, 24>{}); break;

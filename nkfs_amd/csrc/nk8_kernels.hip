@@ -798,9 +798,12 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     if (rc != -ENOSYS)
         return rc;
     // 16 < k <= 32 with digests: the stage-free encoder with a hash wave
-    // (nk8_bign.hip; tune enc_bign)
+    // (nk8_bign.hip; tune enc_bign).  Its units of 8 parts (32 < k <= 76,
+    // pinned with enc_bign 1) lose to the column-chunked encoder + hash
+    // pass: W3 723 / 887, N40K33 762 / 977 GB/s (profiles/r06/ab_bign8_enc.txt)
     const int eb = nkfs_tune_now().enc_bign;
-    if (kern != NKFS_ENC_GENERIC && (eb > 0 || (eb == -1 && digests && g->k > 16 && kern == NKFS_ENC_AUTO))) {
+    if (kern != NKFS_ENC_GENERIC &&
+        (eb > 0 || (eb == -1 && digests && g->k > 16 && g->k <= 32 && kern == NKFS_ENC_AUTO))) {
         rc = nkfs_bign_encode(g, ids, digests, eb != 2, st);
         if (rc != -ENOSYS)
             return rc;
@@ -935,11 +938,20 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     // through an LDS stage (the stage-free one writes such rows bytewise:
     // N40K17 696 / 413, N40K18 736 / 598, N40K33 524 / 523;
     // profiles/r05/ab_oddk.txt)
+    // round 6: rows that are not a dword multiple (16 < k <= 64) take the
+    // all-groups stage-free decoder, whose output goes through an LDS stage
+    // (dec_bign 3, k_decode_bigr): N40K17 696 -> 1,700, N40K33 524 -> 1,095,
+    // W3 N64K41 491 -> 875 GB/s (profiles/r06/ab_bigr_*.txt); k % 4 == 0 keeps
+    // the byte-table form (W2 2,064 vs 1,341).  The automatic choice applies
+    // to NKFS_DEC_AUTO only: a pinned NKFS_DEC_BIG runs the column-chunked
+    // decoder unless dec_bign pins a stage-free layout
     rc = -ENOSYS;
     if (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG) {
-        const bool auto_pick = t.dec_bign == -2 && g->k % 4 == 0 && g->k != 16;
-        if (t.dec_bign >= 0 || auto_pick)
-            rc = nkfs_bign_decode(g, (const u8 *)work, status, t.dec_bign >= 0 ? t.dec_bign : 0, st);
+        int mode = t.dec_bign;
+        if (mode == -2 && t.dec_kernel == NKFS_DEC_AUTO)
+            mode = g->k % 4 == 0 && g->k != 16 ? 0 : g->k > 16 && g->k <= 64 ? 3 : -1;
+        if (mode >= 0)
+            rc = nkfs_bign_decode(g, (const u8 *)work, status, mode, st);
     }
     if (rc == -ENOSYS)
         rc = t.dec_kernel == NKFS_DEC_GENERIC || t.dec_kernel == NKFS_DEC_BIG

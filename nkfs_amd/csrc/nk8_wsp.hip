@@ -126,10 +126,12 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
             r.poff = g.part_off[s];
 #ifdef NKFS_DEBUG_BOUNDS
             // debug-bounds build: report and skip a stripe whose block reads
-            // (dword-rounded) or part stores would leave the caller's buffers
+            // (bytes [boff, boff + B): 16-byte loads only when the whole
+            // 16 K-byte run lies inside B) or part stores would leave the
+            // caller's buffers
             {
                 const u64 pp = (u64(part_size_of(r.B, K)) + NKFS_PART_ALIGN - 1) & ~u64(NKFS_PART_ALIGN - 1);
-                if ((g.blocks_bytes && r.boff + ((u64(r.B) + 3) & ~u64(3)) > g.blocks_bytes) ||
+                if ((g.blocks_bytes && r.boff + u64(r.B) > g.blocks_bytes) ||
                     (g.parts_bytes && r.poff + u64(n) * pp > g.parts_bytes) || (r.poff & 15) ||
                     (g.block_size && r.B > g.block_size) || r.B == 0) {
                     printf("nkfs bounds: k_encode_wsp stripe %u: B %u block [%llu,+%u) of %llu, parts [%llu,+%llu) "

@@ -10,9 +10,10 @@ one and several 16-column chunks, part groups of 16 (the last one partial),
 k = n, k = 254 / n = 255, tails of every size, unaligned ragged offsets,
 one-byte blocks, the small-k shapes pinned to the big kernels, the
 first-k-distinct selection and the -EINVAL stripe.  The stage-free encoder
-with a hash wave (nk8_bign.hip, k_encode_bign: the default for 16 < k <= 32
-with digests; tune enc_bign = 1 pins it for every k <= 32, with or without
-digests) is held to the same cases.
+with a hash wave (nk8_bign.hip, k_encode_bign: the default for 16 < k <= 76
+with digests, in units of 16 parts up to k = 32 and of 8 parts above; tune
+enc_bign = 1 pins it for every k <= 76, with or without digests) is held to
+the same cases.
 """
 import numpy as np
 import pytest
@@ -64,6 +65,12 @@ def _tuned(**kw):
     (24, 20, 65543, 5),        # k % 4 == 0: the stage-free encoder's contiguous row loads, tail row
     (30, 24, 24 * 4096, 4),
     (29, 28, 4099, 9),
+    # 32 < k <= 76: the stage-free encoder in units of 8 parts (8-byte table entries)
+    (64, 41, 1048576, 2),      # the bench's W3 shape
+    (77, 76, 4099, 3),         # the largest k of that encoder, 10 part groups
+    (100, 75, 65537, 2),       # 13 part groups, the last one 4 parts wide
+    (34, 33, 1, 4),            # one-byte blocks
+    (45, 36, 36 * 3840 * 2 + 7, 2),  # k % 4 == 0 above 32, slices + a tail row
 ])
 def test_big_encode_matches(L, O, n, k, B, S):
     from nkfs_amd import _lib, batch
@@ -94,7 +101,7 @@ def test_big_encode_matches(L, O, n, k, B, S):
         assert got[s * n:(s + 1) * n] == [O.xxh64(p) for p in want], s
 
 
-@pytest.mark.parametrize("n,k,gap", [(24, 20, 0), (40, 33, 5), (19, 18, 3), (48, 32, 1)])
+@pytest.mark.parametrize("n,k,gap", [(24, 20, 0), (40, 33, 5), (19, 18, 3), (48, 32, 1), (64, 41, 3), (80, 70, 0)])
 def test_big_encode_ragged(L, O, n, k, gap):
     """Ragged batches (mixed sizes, block offsets unaligned when gap != 0):
     the big kernel equals the general kernel, and the oracle per stripe."""
@@ -143,6 +150,11 @@ def test_big_encode_ragged(L, O, n, k, gap):
     (36, 20, 17 * 1024, 9),
     (16, 12, 65536, 10),       # k <= 16 pinned to the big decoder
     (8, 5, 262144, 6),         # k <= 8 pinned to the big decoder
+    (64, 41, 1048576, 3),      # W3 shape: 3 groups, rows of 41 bytes
+    (12, 9, 65539, 6),         # one group, odd k, tail row
+    (64, 64, 4099, 5),         # 4 groups, k = n = 64
+    (70, 61, 70001, 4),        # 4 groups, the last 13 columns wide
+    (40, 18, 1048576 + 7, 3),  # rows of 18 bytes (dword pairs straddle rows)
 ])
 def test_big_decode_matches(L, O, n, k, B, S):
     """NKFS_DEC_BIG rebuilds every block like the general decoder from k
@@ -164,7 +176,7 @@ def test_big_decode_matches(L, O, n, k, B, S):
     # the column-chunked decoder, then the replicated-table decoder
     # (nk8_bign.hip) in its three table layouts
     for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2),
-                       ("auto", -2)):
+                       ("auto", -2), ("big", 3), ("auto", 3)):
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
@@ -185,6 +197,49 @@ def test_big_decode_matches(L, O, n, k, B, S):
     pn = parts[s * n:(s + 1) * n, :batch.part_size(B, k)].cpu().numpy()
     got = O.decode([pn[j] for j in sel], [int(ids_np[s, j]) for j in sel], k, B)
     assert np.array_equal(np.asarray(got), ref[s].numpy())
+
+
+@pytest.mark.parametrize("n,k,gap", [(24, 17, 0), (40, 33, 5), (64, 41, 3), (48, 32, 1), (12, 11, 7)])
+def test_bigr_decode_ragged(L, O, n, k, gap):
+    """The all-groups stage-free decoder (dec_bign 3: every output column of
+    a slice in one workgroup, rows through an LDS stage) on ragged batches
+    with unaligned block offsets and stripes of 1, k + 1 and 1 MiB bytes:
+    equal to the column-chunked decoder and the general one, blocks exact,
+    bytes between blocks untouched."""
+    from nkfs_amd import _lib, batch
+    sizes = synth.mixed_sizes(14)
+    sizes[:5] = (4096, 1048576, 1, k + 1, 3 * k + 2)
+    boff = np.zeros(len(sizes), np.int64)
+    poff = np.zeros(len(sizes), np.int64)
+    pos, ppos = 0, 0
+    for s, B in enumerate(sizes):
+        boff[s], poff[s] = pos, ppos
+        pos += int(B) + gap
+        ppos += n * batch.part_pitch(int(B), k)
+    host = np.zeros(pos + 16, np.uint8)
+    for s, B in enumerate(sizes):
+        host[boff[s]: boff[s] + B] = synth.stripe_bytes(800 + s, int(B))
+    ids_np = synth.batch_ids(len(sizes), n, first=800)
+    parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
+    batch.encode_ragged(dev(host), dev(boff), dev(sizes.astype(np.int32)), n, k, dev(ids_np), parts, dev(poff), dig,
+                        int(sizes.max()))
+    av = synth.batch_survivors(len(sizes), n, k, first=800)
+    outs = []
+    for kern, mode in (("generic", -1), ("big", -1), ("big", 3), ("auto", 3)):
+        out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+        st = torch.full((len(sizes),), 5, dtype=torch.int32, device="cuda")
+        with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
+            batch.decode_ragged(parts, dev(poff), n, dev(ids_np), dev(av), k, out, dev(boff),
+                                dev(sizes.astype(np.int32)), int(sizes.max()), status=st)
+        torch.cuda.synchronize()
+        outs.append((out.cpu().numpy(), st.cpu().numpy()))
+    blk = np.zeros(pos + 16, bool)
+    for s, B in enumerate(sizes):
+        blk[boff[s]: boff[s] + B] = True
+    for o, st in outs:
+        assert (st == 0).all()
+        assert np.array_equal(o[blk], host[blk]) and (o[~blk] == 0xEE).all()
 
 
 def test_big_round_trip_w2(L, O):
@@ -215,7 +270,7 @@ def test_big_round_trip_w2(L, O):
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     assert torch.equal(out, blocks[:, :B])
-    for mode in (-1, 0, 1, 2):  # the survivor-table decoder, the stage-free one's layouts
+    for mode in (-1, 0, 1, 2, 3):  # the survivor-table decoder, the stage-free one's layouts
         with _tuned(dec_bign=mode):
             out2, status2 = batch.decode(parts, n, ids, avail, k, B)
         torch.cuda.synchronize()
