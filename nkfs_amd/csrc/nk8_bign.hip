@@ -785,6 +785,14 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_DYN
 #define NKFS_BE_DYN 0
 #endif
+// NKFS_BE_BATCH=1 (experiment builds): a column pair's lookups for all 4
+// rows issued before any is folded -- lgkmcnt(6/4/2) waits instead of one
+// per 2 lookups -- lost 4-8 % (W2 1,627 vs 1,776 GB/s,
+// profiles/r06/ab_be_batch.txt): more lookups in flight per wave do not
+// raise this kernel's LDS throughput
+#ifndef NKFS_BE_BATCH
+#define NKFS_BE_BATCH 0
+#endif
 constexpr u32 BE_END = 0xFFFFFFFFu;
 
 // this wave's XCC (hardware register XCC_ID, bits 3:0)
@@ -837,7 +845,11 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 
     const int n = g.n, k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int nch = (k + 15) >> 4;
+    // KC != 0: k == KC, so the column loops' bounds are compile-time (the
+    // runtime bound split every lookup pair into its own basic block, with a
+    // wait for both lookups before the next pair issued)
+    const int kk = KC ? KC : k;
+    const int nch = (kk + 15) >> 4;
     if (tid < BE_WAVES)
         done[tid] = 0;
     if (tid == 0) {
@@ -1037,8 +1049,30 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     u32 tdep = u32(c) * 65536u;
 #pragma unroll
                     for (int j = 0; j < 16; j += 2) {
-                        if (16 * c + j >= k)
+                        if (16 * c + j >= kk)
                             break;  // uniform
+#if NKFS_BE_BATCH
+                        // the pair's 8 lookups (4 rows x 2 columns) issued
+                        // together, then folded: one LDS wait per 8 lookups
+                        // (the per-row form waited for every 2)
+                        uint4 la[4], lb[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
+                            const u32 s1 = 0x0C0C0C00u | u32(4 + ((j + 1) & 3));
+                            const u32 P0 = (__builtin_amdgcn_perm(d[q][j >> 2], 0u, s0) << 4) + tdep;
+                            const u32 P1 = (__builtin_amdgcn_perm(d[q][(j + 1) >> 2], 0u, s1) << 4) + tdep;
+                            la[q] = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
+                            lb[q] = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            acc[q].x = xor3(acc[q].x, la[q].x, lb[q].x);
+                            acc[q].y = xor3(acc[q].y, la[q].y, lb[q].y);
+                            acc[q].z = xor3(acc[q].z, la[q].z, lb[q].z);
+                            acc[q].w = xor3(acc[q].w, la[q].w, lb[q].w);
+                        }
+#else
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
                             const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
@@ -1052,6 +1086,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                             acc[q].z = xor3(acc[q].z, a.z, c2.z);
                             acc[q].w = xor3(acc[q].w, a.w, c2.w);
                         }
+#endif
                         if (j & 2) {
                             u32 z;
                             asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(acc[3].x));

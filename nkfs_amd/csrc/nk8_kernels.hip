@@ -827,7 +827,8 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
-        rc = digests && nkfs_tune_now().enc_big_fused ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
+        const int fz = nkfs_tune_now().enc_big_fused;  // -1 auto: fused for k > 32
+        rc = digests && (fz > 0 || (fz < 0 && g->k > 32)) ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
         if (rc != -ENOSYS)
             return rc;
         rc = nkfs_big_encode(g, ids, nullptr, gf, st);

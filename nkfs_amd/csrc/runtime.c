@@ -68,8 +68,10 @@ static struct nkfs_tune g_tune = {
 	.enc_few_max = 63,
 	.enc_ws_hash_waves = 0, /* auto: 2 from 1,024 stripes (profiles/r04/seam_ws2.txt) */
 	.enc_persist = 1, /* ragged n > 4: C5 encode 4,839 -> 5,051 GB/s (profiles/r05/ab_wsp.txt) */
-	.dec_bign = -2, /* auto: byte tables for k > 16 and k = 12 (profiles/r05/ab_bign.txt) */
+	.dec_bign = -2, /* auto: byte tables for k % 4 == 0 (not 16), all-groups form for the other 16 < k <= 64
+	                 * (profiles/r05/ab_bign.txt, profiles/r06/ab_bigr_*.txt, ab_rule_k*.txt) */
 	.enc_bign = -1,
+	.enc_big_fused = -1, /* auto: XXH64 fused for k > 32 (W3 +4 %, HBM traffic 1.04x; profiles/r06/ab_w3_fused.txt) */
 	.dec_pair_pipe = 0,
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
@@ -95,7 +97,7 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->dec_wave_waves_per_cu && (t->dec_wave_waves_per_cu < 3 || t->dec_wave_waves_per_cu > 32)) ||
 	    (t->dec_run_units != 1 && t->dec_run_units != 2 && t->dec_run_units != 4 && t->dec_run_units != 8 &&
 	     t->dec_run_units != 16) ||
-	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_fused != 0 && t->enc_big_fused != 1) ||
+	    t->enc_ws_prefetch < 1 || t->enc_ws_prefetch > 2 || (t->enc_big_fused < -1 || t->enc_big_fused > 1) ||
 	    (t->dec_pair_stage != 0 && t->dec_pair_stage != 1) || t->host_depth < 2 || t->host_depth > 8 ||
 	    t->host_lanes < 1 || t->host_lanes > 4 || t->enc_ragged_split < 0 ||
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||

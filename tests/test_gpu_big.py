@@ -79,7 +79,7 @@ def test_big_encode_matches(L, O, n, k, B, S):
     ids = dev(ids_np)
     with _tuned(enc_kernel=_lib.ENC["generic"]):
         p0, d0 = batch.encode(blocks, B, n, k, ids)
-    with _tuned(enc_kernel=_lib.ENC["big"]):
+    with _tuned(enc_kernel=_lib.ENC["big"], enc_big_fused=0):  # the XXH64 pass
         p1, d1 = batch.encode(blocks, B, n, k, ids)
     with _tuned(enc_kernel=_lib.ENC["big"], enc_big_fused=1):  # XXH64 fused, chained over the slices
         p3, d3 = batch.encode(blocks, B, n, k, ids)
@@ -120,7 +120,8 @@ def test_big_encode_ragged(L, O, n, k, gap):
         host[boff[s]: boff[s] + B] = synth.stripe_bytes(500 + s, int(B))
     ids_np = synth.batch_ids(len(sizes), n, first=500)
     outs = []
-    for kern, fused, eb in (("generic", 0, 0), ("big", 0, 0), ("big", 1, 0), ("auto", 0, -1), ("auto", 0, 1)):
+    for kern, fused, eb in (("generic", 0, 0), ("big", 0, 0), ("big", 1, 0), ("auto", 0, -1), ("auto", 0, 1),
+                            ("auto", -1, -1)):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
         with _tuned(enc_kernel=_lib.ENC[kern], enc_big_fused=fused, enc_bign=eb):

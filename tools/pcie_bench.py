@@ -3,7 +3,7 @@ the path's real ends, SURVEY.md §8(f) row 2.  User bytes (block bytes) per
 second, host buffers pinned once (a server's page pool), outputs verified
 against the inputs after timing.
 
-    python tools/pcie_bench.py [link c2 c3 c4 c5 pages lanes depth]
+    python tools/pcie_bench.py [link c2 c3 c4 c5 pages lanes depth c2pg c3pg c4pg]
 
 link  = the raw pinned link on this box: hipMemcpyAsync H2D alone, D2H alone,
         and both at once on two streams (1 GiB each way); every PUT / GET line
@@ -11,6 +11,7 @@ link  = the raw pinned link on this box: hipMemcpyAsync H2D alone, D2H alone,
         H2D bytes, the D2H bytes and their sum each fit the measured rates)
         and the fraction of it reached.
 depth = C3 PUT / GET at host_depth 3 / 6 x host_lanes 1 / 2 (struct nkfs_tune)
+c3pg  = C3 from pageable caller buffers (staged through pinned scratch, round 6)
 
 PUT  = nkfs_nk8_encode_host: blocks H2D -> encode + XXH64 -> parts + digests D2H
 GET  = nkfs_nk8_decode_host: k survivor parts per stripe H2D -> decode -> blocks D2H
@@ -104,14 +105,17 @@ def timed(fn, reps=3):
     return (time.perf_counter() - t0) / reps
 
 
-def uniform(name, user_bytes=1 << 30, lanes=None, tune=None):
+def uniform(name, user_bytes=1 << 30, lanes=None, tune=None, pinned=True):
+    """pinned=False: pageable caller buffers, which the library stages
+    through its pinned scratch by host copies (round 6)."""
     S0, B, n, k, _ = CONFIGS[name]
     S = min(S0, user_bytes // B)
     pitch = batch.part_pitch(B, k)
-    blocks = batch.synth(S, B).cpu()[:, :B].contiguous().pin_memory()
-    ids = torch.from_numpy(synth.batch_ids(S, n)).pin_memory()
-    parts = torch.empty((S * n, pitch), dtype=torch.uint8).pin_memory()
-    dig = torch.empty(S * n, dtype=torch.int64).pin_memory()
+    pin = (lambda t: t.pin_memory()) if pinned else (lambda t: t.clone())
+    blocks = pin(batch.synth(S, B).cpu()[:, :B].contiguous())
+    ids = pin(torch.from_numpy(synth.batch_ids(S, n)))
+    parts = pin(torch.empty((S * n, pitch), dtype=torch.uint8))
+    dig = pin(torch.empty(S * n, dtype=torch.int64))
     if lanes is not None:
         _lib.check(batch.set_devices(lanes))
     tune = dict(tune or {})
@@ -123,13 +127,13 @@ def uniform(name, user_bytes=1 << 30, lanes=None, tune=None):
     surv = synth.batch_survivors(S, n, k).astype(np.int64)
     pv = parts.view(S, n, pitch)
     idx = torch.from_numpy(surv)
-    held = torch.gather(pv, 1, idx[:, :, None].expand(S, k, pitch)).contiguous().pin_memory()
-    hid = torch.gather(ids.view(S, n).long(), 1, idx).to(torch.uint8).contiguous().pin_memory()
-    hexp = torch.gather(dig.view(S, n), 1, idx).contiguous().pin_memory()
-    avail = torch.arange(k, dtype=torch.uint8).repeat(S, 1).contiguous().pin_memory()
-    out = torch.empty((S, B), dtype=torch.uint8).pin_memory()
-    st = torch.empty(S, dtype=torch.int32).pin_memory()
-    bad = torch.empty(S, dtype=torch.int64).pin_memory()
+    held = pin(torch.gather(pv, 1, idx[:, :, None].expand(S, k, pitch)).contiguous())
+    hid = pin(torch.gather(ids.view(S, n).long(), 1, idx).to(torch.uint8).contiguous())
+    hexp = pin(torch.gather(dig.view(S, n), 1, idx).contiguous())
+    avail = pin(torch.arange(k, dtype=torch.uint8).repeat(S, 1).contiguous())
+    out = pin(torch.empty((S, B), dtype=torch.uint8))
+    st = pin(torch.empty(S, dtype=torch.int32))
+    bad = pin(torch.empty(S, dtype=torch.int64))
     t_get = timed(lambda: batch.decode_host(held, pitch, k, hid, avail, k, k, B, out, B, status=st, chunk_bytes=chunk))
     ok = bool(torch.equal(out, blocks)) and int(st.abs().sum()) == 0
     t_getv = timed(lambda: batch.decode_host(held, pitch, k, hid, avail, k, k, B, out, B, status=st, expect=hexp,
@@ -140,6 +144,8 @@ def uniform(name, user_bytes=1 << 30, lanes=None, tune=None):
         batch.set_devices([])
     ub = S * B
     tag = f"{name} lanes={lanes}" if lanes is not None else name
+    if not pinned:
+        tag += " pageable"
     if tune or chunk:
         tag += " " + ",".join(f"{a}={b}" for a, b in tune.items()) + (f",chunk={chunk >> 20}M" if chunk else "")
     put, get, getv = ub / t_put / GIB, ub / t_get / GIB, ub / t_getv / GIB
@@ -228,6 +234,8 @@ def main():
                 uniform("c3", tune=tune)
         elif w in ("c2", "c3", "c4"):
             uniform(w)
+        elif w in ("c2pg", "c3pg", "c4pg"):  # pageable caller buffers (staged)
+            uniform(w[:2], pinned=False)
         elif w == "c5":
             ragged()
         elif w == "pages":
