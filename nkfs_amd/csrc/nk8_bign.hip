@@ -793,6 +793,16 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_BATCH
 #define NKFS_BE_BATCH 0
 #endif
+// NKFS_BE_PROG=1 (experiment builds): the hash wave folds each encoder
+// wave's 256-row segment of a slice as soon as that wave has stored it (its
+// own progress count), in chain order, instead of waiting for all 15 waves
+// (test whether the hash wave's lag is what makes its
+// re-read of the parts miss the L2).  It is not: the PMC fetch stayed at 690
+// vs 691 MB per W2 launch (the parts' 403 MB re-fetched either way) and the
+// kernel ran 7-9 % slower (profiles/r06/ab_be_prog.txt, pmc_w2_prog*.txt)
+#ifndef NKFS_BE_PROG
+#define NKFS_BE_PROG 0
+#endif
 constexpr u32 BE_END = 0xFFFFFFFFu;
 
 // this wave's XCC (hardware register XCC_ID, bits 3:0)
@@ -1310,15 +1320,17 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
                 ++seq;
-                for (;;) {
-                    const u32 dv = lane < BE_EW ? __hip_atomic_load(&done[lane], __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)
-                                                : 0xFFFFFFFFu;
-                    if (!__ballot(dv < seq))
-                        break;
-                    __builtin_amdgcn_s_sleep(8);
+                if (!NKFS_BE_PROG) {
+                    for (;;) {
+                        const u32 dv = lane < BE_EW ? __hip_atomic_load(&done[lane], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)
+                                                    : 0xFFFFFFFFu;
+                        if (!__ballot(dv < seq))
+                            break;
+                        __builtin_amdgcn_s_sleep(8);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const u32 rb = sl * (BE_ROWS / 32u);
                 const int re = int(min(rb + BE_ROWS / 32u, nst));
                 // a ring of 4 x 8 rounds: three batches' loads in flight
@@ -1330,6 +1342,15 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 // that slice is folded
                 const u32 rlast = re > int(rb) ? u32(re) - 1u : rb;
                 auto ld = [&](uint64_t (&w)[8], u32 r) {
+                    if (NKFS_BE_PROG) {
+                        // the 8 rounds from r (clamped like the loads) are
+                        // encoder wave (r - rb) / 8's rows of this slice:
+                        // wait for that wave's progress count only
+                        const u32 sw = min((min(r, rlast) - rb) >> 3, u32(BE_EW - 1));
+                        while (__hip_atomic_load(&done[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq)
+                            __builtin_amdgcn_s_sleep(2);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    }
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const u32 ri = min(r + u32(i), rlast);
