@@ -141,13 +141,15 @@ int nkfs_pipeline_check(int decode, const uint64_t *block_off, const uint32_t *b
  * devices (d0, d1, ..., d0, d1, ...) so a cap of max_lanes drops whole
  * rounds, never a device.  Returns the number of lanes written. */
 int nkfs_host_lane_plan(const int *devices, int ndev, int per_device, int *lanes, int max_lanes);
-/* Opt-in per-call service (1 on, 0 off; default off): one wave stays
- * resident on the calling thread's device and polls a mailbox in coherent
- * host memory, so a per-call XXH64 / csum digest of a message up to 256 KiB
+/* Opt-in per-call service (0 off, the default; 1 on, mailbox in coherent
+ * host memory; 2 on, the request half of the mailbox in device memory the
+ * host writes through the PCIe BAR -- needs a host-mapped device aperture):
+ * one wave stays resident on the calling thread's device and polls the
+ * mailbox, so a per-call XXH64 / csum digest of a message up to 256 KiB
  * (XXH64(), csum_digest, XXH64_digest without an earlier 256 KiB fold)
  * needs no kernel launch.  The wave leaves after 20 ms without requests and
- * is relaunched by the next one; requests are serialised.  0, -ENODEV,
- * -ENOMEM or -EIO. */
+ * is relaunched by the next one; requests are serialised.  0, -EINVAL,
+ * -ENODEV, -ENOMEM or -EIO. */
 int nkfs_percall_service(int on);
 
 /* ceil(block_size/k) -- crt/nk8.c:311-317. */

@@ -195,27 +195,49 @@ static int xh_stage(struct xh *h, const uint8_t *p, uint64_t bytes)
  * before.  Requests are serialised by g_svc_lock (one box).  The wave leaves
  * after SVC_IDLE without requests (or SVC_LIFE in all); a request that finds
  * it gone, or that it never took, relaunches it once the service stream has
- * drained. */
+ * drained.
+ *
+ * nkfs_percall_service(2) (round 6): the request half of
+ * the mailbox (seq, op, arguments, inline message) lives in uncached device
+ * memory that the host writes directly through the PCIe BAR (a store
+ * costs the host ~0.23 us, tools/bar_probe.c), so the wave's polls and
+ * argument reads stay on the GPU; only the answer (digest, completion word,
+ * taken, alive: the host-memory half) crosses PCIe to the host.  The host
+ * keeps a shadow of seq, so it never reads device memory (a BAR read costs
+ * ~1.2 us). */
 #define SVC_IDLE 2000000ull      /* s_memrealtime ticks (100 MHz): 20 ms */
 #define SVC_LIFE 1000000000ull   /* 10 s */
 static pthread_mutex_t g_svc_lock = PTHREAD_MUTEX_INITIALIZER;
-static struct nkfs_svc_box *g_svc; /* coherent host memory */
-static struct nkfs_svc_box *g_svc_dev_ptr;
+static struct nkfs_svc_box *g_svc_host, *g_svc_host_dev; /* coherent host memory: the answer half (both modes) */
+static struct nkfs_svc_box *g_svc_bar;                   /* uncached device memory (mode 2), host-mapped */
+static struct nkfs_svc_box *g_svc;                       /* the request half the host writes: host or BAR box */
+static struct nkfs_svc_box *g_svc_in_dev;                /* the same, as the wave sees it */
+static uint64_t g_svc_seq;                               /* the host's shadow of g_svc->seq */
 static hipStream_t g_svc_stream;
-static int g_svc_on, g_svc_device = -1, g_svc_exit_hooked;
+static int g_svc_on, g_svc_mode, g_svc_device = -1, g_svc_exit_hooked;
+
+/* publish the request number after the request (the BAR mapping is
+ * write-combined: the fences keep the payload ahead of seq and push seq) */
+static void svc_post_locked(uint64_t sq)
+{
+	__builtin_ia32_sfence();
+	__atomic_store_n(&g_svc->seq, sq, __ATOMIC_RELEASE);
+	__builtin_ia32_sfence();
+	g_svc_seq = sq;
+}
 
 /* at exit: post a stop and give the wave a bounded time to leave (host
- * memory only: no runtime calls while the process tears down) */
+ * memory and the BAR only: no runtime calls while the process tears down) */
 static void svc_atexit(void)
 {
-	if (!g_svc || !__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE))
+	if (!g_svc || !__atomic_load_n(&g_svc_host->alive, __ATOMIC_ACQUIRE))
 		return;
 	g_svc->op = NKFS_SVC_STOP;
-	__atomic_store_n(&g_svc->seq, g_svc->seq + 1, __ATOMIC_RELEASE);
+	svc_post_locked(g_svc_seq + 1);
 	struct timespec t0, t;
 	clock_gettime(CLOCK_MONOTONIC, &t0);
 	do {
-		if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE))
+		if (!__atomic_load_n(&g_svc_host->alive, __ATOMIC_ACQUIRE))
 			return;
 		clock_gettime(CLOCK_MONOTONIC, &t);
 	} while ((t.tv_sec - t0.tv_sec) * 1000000000ll + (t.tv_nsec - t0.tv_nsec) < 100000000ll);
@@ -223,33 +245,43 @@ static void svc_atexit(void)
 
 static int svc_launch_locked(void)
 {
-	__atomic_store_n(&g_svc->alive, 1, __ATOMIC_RELEASE);
-	int err = nkfs_launch_xxh64_service(g_svc_dev_ptr, SVC_IDLE, SVC_LIFE, g_svc_stream);
+	__atomic_store_n(&g_svc_host->alive, 1, __ATOMIC_RELEASE);
+	int err = nkfs_launch_xxh64_service(g_svc_in_dev, g_svc_host_dev, SVC_IDLE, SVC_LIFE, g_svc_stream);
 	if (err)
-		__atomic_store_n(&g_svc->alive, 0, __ATOMIC_RELEASE);
+		__atomic_store_n(&g_svc_host->alive, 0, __ATOMIC_RELEASE);
 	return err;
+}
+
+/* stop a running wave (a stop uses a request number; the wave marks it
+ * taken) and wait for its stream */
+static int svc_stop_locked(void)
+{
+	if (!g_svc || !__atomic_load_n(&g_svc_host->alive, __ATOMIC_ACQUIRE))
+		return 0;
+	g_svc->op = NKFS_SVC_STOP;
+	svc_post_locked(g_svc_seq + 1);
+	return hipStreamSynchronize(g_svc_stream) != hipSuccess ? -EIO : 0;
 }
 
 int nkfs_percall_service(int on)
 {
+	if (on < 0 || on > 2)
+		return -EINVAL;
 	if (on && ensure_gpu())
 		return -ENODEV;
 	pthread_mutex_lock(&g_svc_lock);
 	int err = 0;
-	if (!on) {
-		if (g_svc && __atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE)) {
-			g_svc->op = NKFS_SVC_STOP;
-			__atomic_store_n(&g_svc->seq, g_svc->seq + 1, __ATOMIC_RELEASE);
-			if (hipStreamSynchronize(g_svc_stream) != hipSuccess)
-				err = -EIO;
-		}
+	if (on && g_svc_on && on == g_svc_mode)
+		goto out; /* already on in this mode: a live wave keeps its counters */
+	if (!on || (g_svc_on && on != g_svc_mode)) {
+		err = svc_stop_locked();
 		__atomic_store_n(&g_svc_on, 0, __ATOMIC_RELEASE);
-		pthread_mutex_unlock(&g_svc_lock);
-		return err;
+		if (!on || err)
+			goto out;
 	}
-	if (!g_svc) {
+	if (!g_svc_host) {
 		void *p = NULL, *dp = NULL;
-		if (hipHostMalloc(&p, sizeof(*g_svc), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+		if (hipHostMalloc(&p, sizeof(*g_svc_host), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
 			err = -ENOMEM;
 			goto out;
 		}
@@ -259,15 +291,38 @@ int nkfs_percall_service(int on)
 			err = -EIO;
 			goto out;
 		}
-		memset(p, 0, sizeof(*g_svc));
-		g_svc = p;
-		g_svc_dev_ptr = dp;
+		memset(p, 0, sizeof(*g_svc_host));
+		g_svc_host = p;
+		g_svc_host_dev = dp;
 		(void)hipGetDevice(&g_svc_device);
 		if (!g_svc_exit_hooked) {
 			g_svc_exit_hooked = 1;
 			atexit(svc_atexit);
 		}
 	}
+	if (on == 2 && !g_svc_bar) {
+		void *d = NULL;
+		/* uncached: the wave's loads of the request never hit a line an
+		 * earlier request left in its L2 (the host's BAR writes go around it) */
+		if (hipExtMallocWithFlags(&d, sizeof(*g_svc_bar), hipDeviceMallocUncached) != hipSuccess ||
+		    hipMemset(d, 0, sizeof(*g_svc_bar)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+			(void)hipGetLastError();
+			if (d)
+				(void)hipFree(d);
+			err = -ENOMEM;
+			goto out;
+		}
+		g_svc_bar = d;
+	}
+	/* a fresh pair of counters for the chosen box: the request number and
+	 * the taken mark start at 0 together (the wave starts from taken) */
+	g_svc = on == 2 ? g_svc_bar : g_svc_host;
+	g_svc_in_dev = on == 2 ? g_svc_bar : g_svc_host_dev;
+	g_svc->seq = 0;
+	__builtin_ia32_sfence();
+	__atomic_store_n(&g_svc_host->taken, 0, __ATOMIC_RELEASE);
+	g_svc_seq = 0;
+	g_svc_mode = on;
 	__atomic_store_n(&g_svc_on, 1, __ATOMIC_RELEASE);
 out:
 	pthread_mutex_unlock(&g_svc_lock);
@@ -310,17 +365,18 @@ static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile 
 	int err = 0;
 	/* the request is complete in the box before its number is published and
 	 * before any (re)launch, so a wave never reads half-written arguments */
-	g_svc->args = *a;
+	struct nkfs_xxh_args ar = *a;
 	/* a message of at most 1 KiB of stripes travels inline: the wave reads
 	 * it in the same round trip as the arguments */
 	if (a->nst * 32 <= NKFS_SVC_INL) {
 		memcpy(g_svc->inl, hsrc, a->nst * 32);
-		g_svc->args.src = g_svc_dev_ptr->inl;
+		ar.src = g_svc_in_dev->inl;
 		g_svc->op = NKFS_SVC_XXH_INL;
 	} else {
 		g_svc->op = NKFS_SVC_XXH;
 	}
-	const uint64_t sq = g_svc->seq + 1;
+	g_svc->args = ar;
+	const uint64_t sq = g_svc_seq + 1;
 	if (g_svc_trace < 0) {
 		g_svc_trace = getenv("NKFS_SVC_TRACE") != NULL;
 		if (g_svc_trace)
@@ -328,12 +384,12 @@ static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile 
 	}
 	const double t0 = g_svc_trace ? mono_us() : 0;
 	double t1 = 0;
-	__atomic_store_n(&g_svc->seq, sq, __ATOMIC_RELEASE);
-	if (!__atomic_load_n(&g_svc->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
+	svc_post_locked(sq);
+	if (!__atomic_load_n(&g_svc_host->alive, __ATOMIC_ACQUIRE) && hipStreamQuery(g_svc_stream) == hipSuccess &&
 	    (err = svc_launch_locked()))
 		goto out;
 	for (uint64_t spin = 0; __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag; spin++) {
-		if (g_svc_trace && !t1 && __atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) == sq)
+		if (g_svc_trace && !t1 && __atomic_load_n(&g_svc_host->taken, __ATOMIC_ACQUIRE) == sq)
 			t1 = mono_us();
 		if ((spin & 0xFFF) == 0xFFF) {
 			/* the service stream's own status, whether or not the wave took
@@ -347,7 +403,7 @@ static int svc_run(const struct nkfs_xxh_args *a, const uint8_t *hsrc, volatile 
 			if (q == hipSuccess && __atomic_load_n(&res[1], __ATOMIC_ACQUIRE) != a->flag) {
 				/* the wave is gone: it left before taking the request
 				 * (relaunch), or took it and never finished (error) */
-				if (__atomic_load_n(&g_svc->taken, __ATOMIC_ACQUIRE) == sq) {
+				if (__atomic_load_n(&g_svc_host->taken, __ATOMIC_ACQUIRE) == sq) {
 					err = -EIO;
 					goto out;
 				}

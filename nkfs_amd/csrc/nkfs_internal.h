@@ -104,10 +104,12 @@ struct nkfs_xxh_args {
 	uint32_t flags;
 };
 int nkfs_launch_xxh64_chain(const struct nkfs_xxh_args *a, void *stream);
-/* Mailbox of the per-call service wave (k_xxh64_service), in coherent host
- * memory: the host writes op and args, then seq (release); the wave copies
- * the args, stores taken = seq, runs the message and stores its completion
- * word; alive drops to 0 when the wave leaves. */
+/* Mailbox of the per-call service wave (k_xxh64_service): the host writes
+ * op and args, then seq (release) into the request box (coherent host
+ * memory, or device memory through the BAR); the wave copies the args,
+ * stores taken = seq into the answer box (host memory), runs the message
+ * and stores its completion word; alive (answer box) drops to 0 when the
+ * wave leaves. */
 #define NKFS_SVC_XXH 1u
 #define NKFS_SVC_STOP 2u
 #define NKFS_SVC_XXH_INL 3u  /* the message's stripes (<= 1 KiB) are in inl */
@@ -120,7 +122,8 @@ struct nkfs_svc_box {
 	uint64_t alive;
 	uint8_t inl[NKFS_SVC_INL] __attribute__((aligned(64)));
 };
-int nkfs_launch_xxh64_service(struct nkfs_svc_box *mb, uint64_t idle_ticks, uint64_t life_ticks, void *stream);
+int nkfs_launch_xxh64_service(struct nkfs_svc_box *mb, struct nkfs_svc_box *ob, uint64_t idle_ticks,
+			      uint64_t life_ticks, void *stream);
 int nkfs_launch_xxh64_batch(const uint8_t *base, const uint64_t *off,
 			    const uint64_t *len, uint32_t count, uint64_t seed,
 			    uint64_t *out, void *stream);

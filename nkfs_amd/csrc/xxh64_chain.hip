@@ -170,10 +170,13 @@ __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
 // `life` ticks in all, or on a stop request, and clears `alive` as it goes:
 // no schedule can leave it running, and the host relaunches it when a
 // request finds it gone.
-__global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle, u64 life)
+// The request half (seq, op, args, inline bytes) is read from `mb` -- host
+// memory, or (mode 2) fine-grained device memory the host writes over the
+// BAR -- and the answer half (taken, alive) written to `ob` in host memory.
+__global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, nkfs_svc_box *ob, u64 idle, u64 life)
 {
     __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
-    u64 last = __hip_atomic_load(&mb->taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    u64 last = __hip_atomic_load(&ob->taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
     u64 tl = t0;
     for (;;) {
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle
                 // wave (which starts from `taken`) sees no request pending
                 // (off -> on left taken one behind seq)
                 if (threadIdx.x == 0)
-                    __hip_atomic_store(&mb->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&ob->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;  // stop
             }
             nkfs_xxh_args a = mb->args;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle
             if (!inl)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unused inline read lands first
             if (threadIdx.x == 0)  // the arguments are taken: the box may be reused
-                __hip_atomic_store(&mb->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&ob->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             chain_run(a, ring, inl);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a message under 32 B left the inline read unused)
             tl = __builtin_amdgcn_s_memrealtime();
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, u64 idle
         __builtin_amdgcn_s_sleep(2);
     }
     if (threadIdx.x == 0)
-        __hip_atomic_store(&mb->alive, u64(0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ob->alive, u64(0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -225,10 +228,11 @@ extern "C" int nkfs_launch_xxh64_chain(const nkfs_xxh_args *a, void *stream)
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-extern "C" int nkfs_launch_xxh64_service(nkfs_svc_box *mb, uint64_t idle_ticks, uint64_t life_ticks, void *stream)
+extern "C" int nkfs_launch_xxh64_service(nkfs_svc_box *mb, nkfs_svc_box *ob, uint64_t idle_ticks, uint64_t life_ticks,
+                                         void *stream)
 {
-    if (!mb)
+    if (!mb || !ob)
         return -EINVAL;
-    hipLaunchKernelGGL(k_xxh64_service, dim3(1), dim3(64), 0, (hipStream_t)stream, mb, idle_ticks, life_ticks);
+    hipLaunchKernelGGL(k_xxh64_service, dim3(1), dim3(64), 0, (hipStream_t)stream, mb, ob, idle_ticks, life_ticks);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -261,3 +261,45 @@ def test_percall_service_off_on(L, O):
         assert crt.xxh64(data) == O.xxh64(data)
     finally:
         assert L.nkfs_percall_service(0) == 0
+    assert L.nkfs_percall_service(3) == -22
+
+
+def test_percall_service_bar_mailbox(L, O):
+    """Mode 2: the request half of the mailbox in
+    uncached device memory written by the host through the BAR.  Back-to-back
+    requests of different messages and lengths (a stale argument or inline
+    byte would show as a wrong digest), a switch to mode 1 and back with the
+    wave live, the idle relaunch, and eight threads at once."""
+    import time
+    from nkfs_amd import crt
+    rng = np.random.default_rng(33)
+    assert L.nkfs_percall_service(2) == 0
+    try:
+        for it in range(60):
+            n = int(rng.integers(0, 3000))
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            assert crt.xxh64(data, it) == O.xxh64(data, it), (it, n)
+        assert L.nkfs_percall_service(1) == 0  # switch with the wave live
+        data = rng.integers(0, 256, 64, dtype=np.uint8)
+        assert crt.xxh64(data) == O.xxh64(data)
+        assert L.nkfs_percall_service(2) == 0
+        assert crt.xxh64(data, 9) == O.xxh64(data, 9)
+        time.sleep(0.1)  # past the idle timeout
+        data = rng.integers(0, 256, 1025, dtype=np.uint8)
+        assert crt.xxh64(data) == O.xxh64(data)
+        datas = [rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8) for _ in range(128)]
+        want = [O.xxh64(d) for d in datas]
+        got = [None] * len(datas)
+
+        def work(t):
+            for i in range(t, len(datas), 8):
+                got[i] = crt.xxh64(datas[i])
+
+        th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert got == want
+    finally:
+        assert L.nkfs_percall_service(0) == 0

@@ -93,11 +93,12 @@ int main(int argc, char **argv)
 		fprintf(stderr, "nk8_init failed\n");
 		return 1;
 	}
-	/* PERCALL_SVC=1: the product's opt-in resident service wave for the
-	 * per-call digests (nkfs_percall_service; absent in the reference) */
+	/* PERCALL_SVC=1 / 2: the product's opt-in resident service wave for
+	 * the per-call digests, mailbox in host memory / in device memory
+	 * written over the BAR (nkfs_percall_service; absent in the reference) */
 	if (getenv("PERCALL_SVC")) {
 		int (*svc)(int) = (int (*)(int))dlsym(h, "nkfs_percall_service");
-		if (!svc || svc(1)) {
+		if (!svc || svc(atoi(getenv("PERCALL_SVC")))) {
 			fprintf(stderr, "nkfs_percall_service unavailable\n");
 			return 1;
 		}
