@@ -506,7 +506,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
     constexpr int CW = SH::CW, NT = SH::NT, KP = SH::KMAX;
     __shared__ __attribute__((aligned(16))) u8 tbl[CW * 4096];  // tables; the output stage after the lookups
     __shared__ __attribute__((aligned(16))) u8 wl[SH::WL];      // wl[c * KP + m] = W[c][m], 0 for m >= k
-    __shared__ u32 wsoff[KP];                                   // survivor c's part offset (slot * pitch)
+    __shared__ __attribute__((aligned(16))) u32 wsoff[KP];     // survivor c's part offset (slot * pitch), 0 past k
 
     const u32 b = blockIdx.x;
     const u32 s = b / nwg, wi = b % nwg;
@@ -531,16 +531,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
     // survivor loads: slot offsets from LDS at each chunk's load (PAL: one
     // buffer resource over the stripe's slots, the launcher checks n * pitch
     // < 2^31; otherwise clamped byte loads)
+    // All CW loads are issued, branch-free (survivors past k read slot 0's
+    // rows and are never looked up): a runtime break per survivor split the
+    // loads into a chain of blocks, each load waited for (vmcnt(0)) and
+    // spilled before the next one issued -- 14 VGPRs of scratch traffic per
+    // slice, ~25 % of the W3 decode's HBM bytes (profiles/r06/pmc_w3_summary.txt)
     auto load = [&](u32 (&d)[CW], u32 r4, int cc) {
+        if constexpr (NG >= 4) {  // (branch-free, NG = 4 spilled 1,292 VGPRs: the old form)
+#pragma unroll
+            for (int j = 0; j < CW; ++j) {
+                if (CW * cc + j >= k)
+                    break;  // uniform
+                const u32 so = __builtin_amdgcn_readfirstlane(wsoff[CW * cc + j]);
+                if constexpr (PAL)
+                    d[j] = __builtin_amdgcn_raw_buffer_load_b32(prs, so + r4, 0, 0);
+                else
+                    d[j] = r4 < v.ps ? load4_any(v.parts + so + r4, v.ps - r4) : 0u;
+            }
+            return;
+        }
+        u32 so[CW];
+#pragma unroll
+        for (int i = 0; i < CW / 4; ++i) {
+            const uint4 o4 = reinterpret_cast<const uint4 *>(wsoff + CW * cc)[i];
+            so[4 * i] = __builtin_amdgcn_readfirstlane(o4.x);
+            so[4 * i + 1] = __builtin_amdgcn_readfirstlane(o4.y);
+            so[4 * i + 2] = __builtin_amdgcn_readfirstlane(o4.z);
+            so[4 * i + 3] = __builtin_amdgcn_readfirstlane(o4.w);
+        }
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
-            if (CW * cc + j >= k)
-                break;  // uniform: survivors past k are never looked up
-            const u32 so = __builtin_amdgcn_readfirstlane(wsoff[CW * cc + j]);
             if constexpr (PAL)
-                d[j] = __builtin_amdgcn_raw_buffer_load_b32(prs, so + r4, 0, 0);
+                d[j] = __builtin_amdgcn_raw_buffer_load_b32(prs, r4, so[j], 0);
             else
-                d[j] = r4 < v.ps ? load4_any(v.parts + so + r4, v.ps - r4) : 0u;
+                d[j] = r4 < v.ps ? load4_any(v.parts + so[j] + r4, v.ps - r4) : 0u;
         }
     };
     // one row quad: the chunk's survivors' products for group h into a4
@@ -628,6 +652,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
             load(d[0][t], r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u, 0);
 #pragma unroll
         for (int cc = 0; cc < NG; ++cc) {
+            // the chunk's loads stay at the chunk: without this the
+            // branch-free loads of all NG chunks were hoisted to the top of
+            // the slice (NG = 4: 1,292 VGPRs spilled)
+            asm volatile("" ::: "memory");
             if (!BR_PREFETCH && cc > 0)
 #pragma unroll
                 for (int t = 0; t < T; ++t)
