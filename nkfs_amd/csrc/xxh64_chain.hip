@@ -45,9 +45,13 @@ constexpr int NS = 32;
 __device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring, bool pre = false)
 {
     const int li = threadIdx.x, lane = li & 3;
-    // (selects, not a.v[lane]: a dynamically indexed kernel argument goes
-    // through scratch)
-    u64 acc = lane == 0 ? a.v[0] : lane == 1 ? a.v[1] : lane == 2 ? a.v[2] : a.v[3];
+    // (selects, not a.v[lane]: a dynamically indexed argument goes through
+    // scratch -- a memory round trip before the first round.  The compiler
+    // folds a select chain over a.v back into that index, so the four
+    // values are made opaque first)
+    u64 w0 = a.v[0], w1 = a.v[1], w2 = a.v[2], w3 = a.v[3];
+    asm volatile("" : "+s"(w0), "+s"(w1), "+s"(w2), "+s"(w3));
+    u64 acc = lane == 0 ? w0 : lane == 1 ? w1 : lane == 2 ? w2 : w3;
     if (a.flags & NKFS_XXH_FROM_DEV)
         acc = a.v_dev[lane];
     const u64 nst = a.nst;
@@ -126,14 +130,23 @@ __device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring, bool
     const u64 v3 = __shfl(acc, 2, 64), v4 = __shfl(acc, 3, 64);
     if (threadIdx.x != 0)
         return;
+    // The answer words are written through to memory (system-scope stores)
+    // and the completion word follows once they are acknowledged: the
+    // ordering a release would give, without its write-back of the whole L2
+    // before the completion word (these kernels leave nothing else in it)
+    auto put = [](u64 *p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    auto complete = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        put(a.out + 1, a.flag);
+    };
     if (a.flags & NKFS_XXH_EMIT) {  // the accumulators back to the host state
-        a.out[2] = v1;
-        a.out[3] = v2;
-        a.out[4] = v3;
-        a.out[5] = v4;
+        put(a.out + 2, v1);
+        put(a.out + 3, v2);
+        put(a.out + 4, v3);
+        put(a.out + 5, v4);
     }
     if (!(a.flags & NKFS_XXH_FINISH)) {
-        __hip_atomic_store(a.out + 1, a.flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        complete();
         return;
     }
     // merge (crt/xxhash.c:849-877), length (:884), tail (:886-910),
@@ -150,9 +163,8 @@ __device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring, bool
         tw[w] = x;
     }
     const u64 dig = xxh_tail_regs(h, tw, a.tail_len);
-    a.out[0] = dig;
-    // the completion word after the digest, visible to the host in order
-    __hip_atomic_store(a.out + 1, a.flag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    put(a.out, dig);
+    complete();  // the completion word after the digest, visible in order
 }
 
 __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
@@ -187,7 +199,15 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, nkfs_svc
             // same round trip as the arguments
             __builtin_amdgcn_global_load_lds((const void *)(mb->inl + 16 * threadIdx.x),
                                              (__attribute__((address_space(3))) void *)ring, 16, 0, 0);
+            // op and the arguments in the same round trip as the inline bytes
+            // (all three are complete before seq is published); the branch on
+            // op waits for all of them at once.  (The clobber keeps the
+            // argument loads behind the inline read: scheduled first, the
+            // read waited for one of them before it was issued.)
+            asm volatile("" ::: "memory");
             const u64 op = mb->op;
+            nkfs_xxh_args a = mb->args;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (op != NKFS_SVC_XXH && op != NKFS_SVC_XXH_INL) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 // a stop uses a request number too: mark it taken, so the next
@@ -197,12 +217,15 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, nkfs_svc
                     __hip_atomic_store(&ob->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;  // stop
             }
-            nkfs_xxh_args a = mb->args;
             const bool inl = op == NKFS_SVC_XXH_INL;
             if (!inl)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unused inline read lands first
-            if (threadIdx.x == 0)  // the arguments are taken: the box may be reused
-                __hip_atomic_store(&ob->taken, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the arguments are in registers (lgkmcnt(0) above): the box may be
+            // reused.  A relaxed store -- a release here would write back the
+            // L2 and wait for it before the chain starts; the host reads
+            // `taken` only to tell a lost wave from a slow one
+            if (threadIdx.x == 0)
+                __hip_atomic_store(&ob->taken, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             chain_run(a, ring, inl);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a message under 32 B left the inline read unused)
             tl = __builtin_amdgcn_s_memrealtime();
