@@ -117,7 +117,9 @@ struct nkfs_tune {
 	                         parts up to k = 32, of 8 parts above): -1 = auto
 	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64
 	                         pass), 1 = every k <= 76 batch it accepts, persistent (a workgroup per CU walking
-	                         the (stripe, part group) units), 2 = the same, one workgroup per unit */
+	                         the (stripe, part group) units), 2 = the same, one workgroup per unit, 3 = the
+	                         VALU encoder for every k (nk8_vp.hip: products by v_perm from 2-bit tables in scalar
+	                         registers, no LDS tables) */
 	int dec_pair_pipe;    /* k = 2 decode of uniform batches of blocks <= 4 KiB (C2): waves per CU of the persistent
 	                         pipelined pair decoder (next stripes' slots, ids and parts in flight under the current
 	                         one), taken automatically when > 0; 0 = the wave decoder */

@@ -85,6 +85,16 @@ __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
     return r;
 }
 
+// mask ? a : b per bit in one v_bitop3_b32 (operand truth tables S0 0xF0,
+// S1 0xCC, S2 0xAA: (S2 & S0) | (~S2 & S1) = 0xE4); the compiler turns the
+// C form into a v_cndmask on an SGPR lane mask (half rate)
+__device__ __forceinline__ u32 mux3(u32 mask, u32 a, u32 b)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xE4" : "=v"(r) : "v"(a), "v"(b), "v"(mask));
+    return r;
+}
+
 __device__ __forceinline__ u32 load4_any(const u8 *p, u32 left)
 {
     u32 w = 0;
@@ -831,6 +841,16 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_PROG
 #define NKFS_BE_PROG 0
 #endif
+// NKFS_BE_HPRIO (experiment builds): the hash wave's s_setprio level (its
+// XXH64 chain is latency-bound and shares each SIMD with busy encoder waves)
+// NKFS_BE_HW (experiment builds): hash waves per workgroup (1, or 2 taking
+// alternate units)
+#ifndef NKFS_BE_HW
+#define NKFS_BE_HW 1
+#endif
+#ifndef NKFS_BE_HPRIO
+#define NKFS_BE_HPRIO 0
+#endif
 constexpr u32 BE_END = 0xFFFFFFFFu;
 
 // this wave's XCC (hardware register XCC_ID, bits 3:0)
@@ -848,9 +868,10 @@ struct BeShape {
 };
 
 // barrier of the encoder waves only (LDS counter; the hash wave runs on)
+template <int EW>
 __device__ __forceinline__ void enc_barrier(u32 *bar, u32 &gen, int lane)
 {
-    gen += BE_EW;
+    gen += EW;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     if (lane == 0)
         __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -867,19 +888,25 @@ __device__ __forceinline__ u32 be_stripe(u32 u, u32 ngroups, u32 &grp)
     return (loc / ngroups) * 8 + (u & 7);
 }
 
-template <int P, bool HASH, int KC>
+template <int P, bool HASH, int KC, bool DIAG, int HWV>
 __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, const u8 *ids, u64 *digests,
                                                                    u32 ngroups, u32 nunits, u32 *uctr)
 {
     static_assert(P == 16 || (P == 8 && KC == 0), "part groups of 16, or of 8 without contiguous-row loads");
+    static_assert(!DIAG || P == 16, "diagonal tables: units of 16 parts");
+    // HWV hash waves (1 or 2: units alternate between them), EW encoders
+    static_assert(HWV == 1 || HWV == 2, "one or two hash waves");
+    constexpr int EW = BE_WAVES - HWV;
+    constexpr u32 ROWS = 64u * EW * 4u;  // rows per slice (3,840 or 3,584: 120 or 112 XXH64 rounds)
     constexpr u32 TB = BeShape<P>::TB;
     constexpr int TPW = 64 / P;  // tables whose Vandermonde row one wave computes per pass
     __shared__ __attribute__((aligned(16))) u8 tbl[BeShape<P>::CMAX * TB];
+    __shared__ __attribute__((aligned(16))) u8 vrow[DIAG ? 2 * 16 * 16 : 16];  // DIAG: the Vandermonde rows
     __shared__ u32 done[BE_WAVES];  // slices stored so far, per encoder wave
     __shared__ u32 bar;
     __shared__ u32 uq[8];           // NKFS_BE_DYN: the workgroup's claimed units, in order
     __shared__ u32 uq_n, hdone;     // claims published / units the hash wave finished
-    const bool dyn = NKFS_BE_DYN && uctr;
+    const bool dyn = NKFS_BE_DYN && uctr && HWV == 1;
 
     const int n = g.n, k = g.k;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -897,13 +924,13 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
     }
     __syncthreads();
 
-    if (wave < BE_EW) {
+    if (wave < EW) {
         u32 gen = 0, seq = 0;
 #pragma unroll 1
         for (u32 ci = 0;; ++ci) {
             u32 u;
             if (dyn) {
-                enc_barrier(&bar, gen, lane);  // the previous unit's lookups are done
+                enc_barrier<EW>(&bar, gen, lane);  // the previous unit's lookups are done
                 if (wave == 0) {
                     // at most 8 claims ahead of the hash wave (the uq ring)
                     while (ci >= __hip_atomic_load(&hdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 8u)
@@ -923,7 +950,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         __hip_atomic_store(&uq_n, ci + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
-                enc_barrier(&bar, gen, lane);  // the claim is visible
+                enc_barrier<EW>(&bar, gen, lane);  // the claim is visible
                 u = uq[ci % 8];
                 if (u == BE_END)
                     break;
@@ -940,7 +967,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const int p0 = int(grp) * P, np = min(P, n - p0);
 
             // every encoder wave is done with the previous unit's tables
-            enc_barrier(&bar, gen, lane);
+            enc_barrier<EW>(&bar, gen, lane);
             // Vandermonde rows of the group's parts, x^m by square and
             // multiply (crt/nk8.c:404-406 builds the same powers by repeated
             // multiplication): lane 16t + e computes byte e of the wave's
@@ -950,7 +977,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             // wave + 105 >= 76)
             u32 xb;
             {
-                const int t = lane / P, e = lane % P, m = wave + BE_EW * t;
+                const int t = lane / P, e = lane % P, m = wave + EW * t;
                 u32 r = 0;
                 if (e < np && m < k && (P == 8 || t < 3)) {
                     u32 x = ids[u64(s) * u64(n) + u64(p0 + e)];
@@ -964,9 +991,48 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 }
                 xb = r;
             }
+            if constexpr (DIAG) {
+                // diagonal layout: entry x of column m at (m >> 4) * 64 KiB +
+                // x * 256 + (m & 15) * 16, so the 16 columns of a chunk sit in
+                // the 16 bank slots of each 256-byte x row.  The rows go
+                // through the LDS; then wave 4c + qt builds x = xl + 4 s + 64
+                // qt of chunk c's 16 tables, lane 16 xl + j its table j:
+                // the 8 lanes of a ds_write_b128 group write 8 bank slots of
+                // one x row (no conflict)
+                {
+                    const int t = lane / 16, e = lane % 16, m = wave + EW * t;
+                    if (t < 3 && m < 16 * nch)
+                        vrow[m * 16 + e] = u8(xb);
+                }
+                enc_barrier<EW>(&bar, gen, lane);
+                if (wave < 4 * nch) {
+                    const int c = wave >> 2, qt = wave & 3, j = lane & 15, xl = lane >> 4;
+                    const uint4 rv = *reinterpret_cast<const uint4 *>(vrow + (16 * c + j) * 16);
+                    const u32 row[4] = {rv.x, rv.y, rv.z, rv.w};
+                    u32 basis[8][4];
+                    make_basis<4>(basis, row);
+                    u32 hv[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        hv[w] = (basis[0][w] & (0u - u32(xl & 1))) ^ (basis[1][w] & (0u - u32(xl >> 1))) ^
+                                (basis[6][w] & (0u - u32(qt & 1))) ^ (basis[7][w] & (0u - u32(qt >> 1)));
+                    u8 *tb = tbl + u32(c) * 65536u + u32(j) * 16u;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        if (i) {
+                            const int bit = __builtin_ctz(i);
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                hv[w] ^= basis[2 + bit][w];
+                        }
+                        const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 64u * u32(qt);
+                        *reinterpret_cast<uint4 *>(tb + x * 256u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+                    }
+                }
+            }
 #pragma unroll 1
-            for (int t = 0; t < (P == 16 ? 3 : TPW); ++t) {
-                const int m = wave + BE_EW * t;
+            for (int t = 0; t < (DIAG ? 0 : P == 16 ? 3 : TPW); ++t) {
+                const int m = wave + EW * t;
                 // P = 16: columns k .. 16 nch - 1 get zero tables (lookups in
                 // column pairs); P = 8: only columns < k exist -- 16 nch
                 // tables would overrun the LDS at k = 76 -- and a pair's
@@ -995,7 +1061,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         *reinterpret_cast<uint4 *>(tbl + m * TB + (lane + 64 * i) * 16) = make_uint4(0, 0, 0, 0);
                 }
             }
-            enc_barrier(&bar, gen, lane);
+            enc_barrier<EW>(&bar, gen, lane);
 
             if constexpr (P == 16) {
             // the block through a buffer resource based at the dword below
@@ -1004,8 +1070,25 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<u8 *>(v.blk - mis), (short)0, int((v.B + mis + 3u) & ~3u), 0x00020000);
-            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 nsl = (v.ps + ROWS - 1) / ROWS;
             const u32 rl = u32(wave * 64 + lane) * 4u;
+            // DIAG: lane l walks a chunk's columns from (l & 15): its row
+            // bytes rotated by r = l & 15 (dword rotation by two bit-field
+            // selects, byte rotation by v_alignbyte), and step j's address
+            // = x * 256 + slot((j + r) & 15), the slot bytes held in slot4[]:
+            // the 16 lanes of every b128 lane group ({0-3,12-15,20-27}, ...:
+            // distinct l & 15) read 16 distinct bank slots
+            const u32 r16 = u32(lane & 15);
+            const u32 mk2 = (r16 & 8u) ? ~0u : 0u, mk1 = (r16 & 4u) ? ~0u : 0u, rb = r16 & 3u;
+            u32 slot4[4];
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                u32 x = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    x |= (((u32(4 * gq + i) + r16) & 15u) << 4) << (8 * i);
+                slot4[gq] = x;
+            }
             // every chunk's bytes of a slice's 4 rows, all loads in flight at
             // once: KC (k % 4 == 0, dword-aligned block) the 4k contiguous
             // bytes of the lane's rows in k/4 16-byte loads; otherwise per
@@ -1045,7 +1128,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             load(rl);
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
-                const u32 r0 = sl * BE_ROWS + rl;
+                const u32 r0 = sl * ROWS + rl;
                 const bool last = sl + 1 == nsl;
                 uint4 acc[4];
 #pragma unroll
@@ -1082,13 +1165,28 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                             }
                         }
                     }
+                    if constexpr (DIAG) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            u32 a[4], b[4];
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                a[w] = mux3(mk2, d[q][(w + 2) & 3], d[q][w]);
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                b[w] = mux3(mk1, a[(w + 1) & 3], a[w]);
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                d[q][w] = __builtin_amdgcn_alignbyte(b[(w + 1) & 3], b[w], rb);
+                        }
+                    }
                     // columns in pairs (one three-input XOR per word folds
                     // both); tdep (0 at run time) keeps 16 lookups in flight
                     u32 tdep = u32(c) * 65536u;
 #pragma unroll
                     for (int j = 0; j < 16; j += 2) {
-                        if (16 * c + j >= kk)
-                            break;  // uniform
+                        if (!DIAG && 16 * c + j >= kk)
+                            break;  // uniform (DIAG: every step, columns past k meet zero tables)
 #if NKFS_BE_BATCH
                         // the pair's 8 lookups (4 rows x 2 columns) issued
                         // together, then folded: one LDS wait per 8 lookups
@@ -1096,12 +1194,21 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         uint4 la[4], lb[4];
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
+                            if constexpr (DIAG) {
+                                const u32 t0 = 0x0C0C0004u | (u32(j & 3) << 8) | u32(j & 3);
+                                const u32 t1 = 0x0C0C0004u | (u32((j + 1) & 3) << 8) | u32((j + 1) & 3);
+                                const u32 P0 = __builtin_amdgcn_perm(slot4[j >> 2], d[q][j >> 2], t0) + tdep;
+                                const u32 P1 = __builtin_amdgcn_perm(slot4[(j + 1) >> 2], d[q][(j + 1) >> 2], t1) + tdep;
+                                la[q] = *reinterpret_cast<const uint4 *>(tbl + P0);
+                                lb[q] = *reinterpret_cast<const uint4 *>(tbl + P1);
+                            } else {
                             const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
                             const u32 s1 = 0x0C0C0C00u | u32(4 + ((j + 1) & 3));
                             const u32 P0 = (__builtin_amdgcn_perm(d[q][j >> 2], 0u, s0) << 4) + tdep;
                             const u32 P1 = (__builtin_amdgcn_perm(d[q][(j + 1) >> 2], 0u, s1) << 4) + tdep;
                             la[q] = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
                             lb[q] = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
+                            }
                         }
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
@@ -1113,12 +1220,23 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 #else
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
+                            uint4 a, c2;
+                            if constexpr (DIAG) {
+                                // byte 0: the slot of column (j + r) & 15, byte 1: x
+                                const u32 t0 = 0x0C0C0004u | (u32(j & 3) << 8) | u32(j & 3);
+                                const u32 t1 = 0x0C0C0004u | (u32((j + 1) & 3) << 8) | u32((j + 1) & 3);
+                                const u32 P0 = __builtin_amdgcn_perm(slot4[j >> 2], d[q][j >> 2], t0) + tdep;
+                                const u32 P1 = __builtin_amdgcn_perm(slot4[(j + 1) >> 2], d[q][(j + 1) >> 2], t1) + tdep;
+                                a = *reinterpret_cast<const uint4 *>(tbl + P0);
+                                c2 = *reinterpret_cast<const uint4 *>(tbl + P1);
+                            } else {
                             const u32 s0 = 0x0C0C0C00u | u32(4 + (j & 3));
                             const u32 s1 = 0x0C0C0C00u | u32(4 + ((j + 1) & 3));
                             const u32 P0 = (__builtin_amdgcn_perm(d[q][j >> 2], 0u, s0) << 4) + tdep;
                             const u32 P1 = (__builtin_amdgcn_perm(d[q][(j + 1) >> 2], 0u, s1) << 4) + tdep;
-                            const uint4 a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
-                            const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
+                            a = *reinterpret_cast<const uint4 *>(tbl + u32(j) * 4096u + P0);
+                            c2 = *reinterpret_cast<const uint4 *>(tbl + u32(j + 1) * 4096u + P1);
+                            }
                             acc[q].x = xor3(acc[q].x, a.x, c2.x);
                             acc[q].y = xor3(acc[q].y, a.y, c2.y);
                             acc[q].z = xor3(acc[q].z, a.z, c2.z);
@@ -1134,7 +1252,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 }
                 // (NKFS_BE_LATE_LOAD 0: the next slice's loads before the stores)
                 if (!NKFS_BE_LATE_LOAD && !last)
-                    load(r0 + BE_ROWS);
+                    load(r0 + ROWS);
                 // row quad -> one dword of 4 rows per part
                 if (r0 < v.ps) {
 #pragma unroll
@@ -1167,23 +1285,23 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     if constexpr (NKFS_BE_LATE_LOAD && KC != 0) {
                         // the KC/4 loads of the next slice may stay in flight
                         if (!last) {
-                            load(r0 + BE_ROWS);
+                            load(r0 + ROWS);
                             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KC / 4) : "memory");
                         } else {
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         }
                     } else {
                         if (NKFS_BE_LATE_LOAD && !last)
-                            load(r0 + BE_ROWS);
+                            load(r0 + ROWS);
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                     ++seq;
                     if (lane == 0)
                         __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (NKFS_BE_SLICE_BAR)
-                        enc_barrier(&bar, gen, lane);
+                        enc_barrier<EW>(&bar, gen, lane);
                 } else if (NKFS_BE_LATE_LOAD && !last) {
-                    load(r0 + BE_ROWS);
+                    load(r0 + ROWS);
                 }
             }
             } else {
@@ -1197,7 +1315,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<u8 *>(v.blk - mis), (short)0, int((v.B + mis + 3u) & ~3u), 0x00020000);
-            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 nsl = (v.ps + ROWS - 1) / ROWS;
             const u32 rl = u32(wave * 64 + lane) * 4u;
             constexpr int NCH = (BE_CMAX8 + 15) / 16;
             u32 raw[2][4][5];
@@ -1216,7 +1334,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             load(raw[0], rl, 0);
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
-                const u32 r0 = sl * BE_ROWS + rl;
+                const u32 r0 = sl * ROWS + rl;
                 const bool last = sl + 1 == nsl;
                 uint2 acc[4];
 #pragma unroll
@@ -1298,7 +1416,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 if constexpr (HASH) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     if (!last) {
-                        load(raw[0], r0 + BE_ROWS, 0);
+                        load(raw[0], r0 + ROWS, 0);
                         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                     } else {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1307,12 +1425,14 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     if (lane == 0)
                         __hip_atomic_store(&done[wave], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else if (!last) {
-                    load(raw[0], r0 + BE_ROWS, 0);
+                    load(raw[0], r0 + ROWS, 0);
                 }
             }
             }
         }
     } else if constexpr (HASH) {
+        if (NKFS_BE_HPRIO)
+            __builtin_amdgcn_s_setprio(NKFS_BE_HPRIO);
         const int e = lane >> 2, a = lane & 3;
         u32 seq = 0;
 #pragma unroll 1
@@ -1337,7 +1457,11 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 continue;
             const Stripe v = stripe_at(g, s);
             const int p0 = int(grp) * P, np = min(P, n - p0);  // P = 8: lanes 32.. idle (their e >= np)
-            const u32 nsl = (v.ps + BE_ROWS - 1) / BE_ROWS;
+            const u32 nsl = (v.ps + ROWS - 1) / ROWS;
+            if (HWV == 2 && int(ci & 1u) != wave - EW) {
+                seq += nsl;  // the other hash wave's unit
+                continue;
+            }
             const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
             // the group's parts through one buffer resource (the launcher
             // checks n * pitch < 2^31); loads bypass the CU's L1 (sc0)
@@ -1350,7 +1474,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 ++seq;
                 if (!NKFS_BE_PROG) {
                     for (;;) {
-                        const u32 dv = lane < BE_EW ? __hip_atomic_load(&done[lane], __ATOMIC_RELAXED,
+                        const u32 dv = lane < EW ? __hip_atomic_load(&done[lane], __ATOMIC_RELAXED,
                                                                         __HIP_MEMORY_SCOPE_WORKGROUP)
                                                     : 0xFFFFFFFFu;
                         if (!__ballot(dv < seq))
@@ -1359,8 +1483,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
-                const u32 rb = sl * (BE_ROWS / 32u);
-                const int re = int(min(rb + BE_ROWS / 32u, nst));
+                const u32 rb = sl * (ROWS / 32u);
+                const int re = int(min(rb + ROWS / 32u, nst));
                 // a ring of 4 x 8 rounds: three batches' loads in flight
                 // while one is folded (the chain is bound by its serial
                 // rounds, ~35 ns each, not by the L2's latency).  Loads past
@@ -1374,7 +1498,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         // the 8 rounds from r (clamped like the loads) are
                         // encoder wave (r - rb) / 8's rows of this slice:
                         // wait for that wave's progress count only
-                        const u32 sw = min((min(r, rlast) - rb) >> 3, u32(BE_EW - 1));
+                        const u32 sw = min((min(r, rlast) - rb) >> 3, u32(EW - 1));
                         while (__hip_atomic_load(&done[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < seq)
                             __builtin_amdgcn_s_sleep(2);
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1463,7 +1587,7 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
 // (stripe, part group).  -ENOSYS when the shape is outside
 // what it handles (the caller takes the column-chunked encoder).
 extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool persist,
-                                hipStream_t st)
+                                bool diag, hipStream_t st)
 {
     const int k = g->k, n = g->n;
     if (k < 2 || k > BE_CMAX8 || n < k || g->part_min || g->part_max)
@@ -1504,12 +1628,16 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         }
     }
     auto go = [&](auto hash, auto kcon) {
-        hipLaunchKernelGGL((k_encode_bign<16, decltype(hash)::value, decltype(kcon)::value>), dim3(grid),
-                           dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
+        if (diag)
+            hipLaunchKernelGGL((k_encode_bign<16, decltype(hash)::value, decltype(kcon)::value, true, NKFS_BE_HW>), dim3(grid),
+                               dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
+        else
+            hipLaunchKernelGGL((k_encode_bign<16, decltype(hash)::value, decltype(kcon)::value, false, NKFS_BE_HW>), dim3(grid),
+                               dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
     };
     auto pick = [&](auto hash) {
         if (P == 8) {
-            hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
+            hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0, false, 1>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
                                *g, ids, digests, u32(ngroups), u32(nunits), uctr);
             return;
         }

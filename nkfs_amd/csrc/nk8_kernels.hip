@@ -672,7 +672,8 @@ extern "C" int nkfs_big_decode(const nkfs_geom *g, const uint8_t *work, const in
 extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int mode,
                                 hipStream_t st);
 extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool persist,
-                                hipStream_t st);
+                                bool diag, hipStream_t st);
+extern "C" int nkfs_vp_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
@@ -802,11 +803,20 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     // pinned with enc_bign 1) lose to the column-chunked encoder + hash
     // pass: W3 723 / 887, N40K33 762 / 977 GB/s (profiles/r06/ab_bign8_enc.txt)
     const int eb = nkfs_tune_now().enc_bign;
-    if (kern != NKFS_ENC_GENERIC &&
-        (eb > 0 || (eb == -1 && digests && g->k > 16 && g->k <= 32 && kern == NKFS_ENC_AUTO))) {
-        rc = nkfs_bign_encode(g, ids, digests, eb != 2, st);
+    // enc_bign 3: the VALU encoder (nk8_vp.hip: products by v_perm from
+    // 2-bit tables in scalar registers, no LDS tables), any k
+    if (kern != NKFS_ENC_GENERIC && eb == 3) {
+        rc = nkfs_vp_encode(g, ids, digests, st);
         if (rc != -ENOSYS)
             return rc;
+    }
+    if (kern != NKFS_ENC_GENERIC && eb != 3 &&
+        (eb > 0 || (eb == -1 && digests && g->k > 16 && g->k <= 32 && kern == NKFS_ENC_AUTO))) {
+        // enc_bign 5 (experiment): diagonal tables without the hash wave,
+        // then the batched XXH64 pass over the parts
+        rc = nkfs_bign_encode(g, ids, eb == 5 ? nullptr : digests, eb != 2, eb >= 4, st);
+        if (rc != -ENOSYS)
+            return rc || eb != 5 || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
     }
     // n > 8 (or a few big stripes), k <= 16: with digests and a batch that
     // fills the chip (two workgroups of 16 parts per CU), the part-group

@@ -40,6 +40,10 @@ using namespace nkfs::dev;
 
 // SB: single-buffered exchange (the hash wave copies its words to registers
 // between two barriers per chunk) -- half the LDS, so more workgroups per CU
+// NKFS_WS_HPRIO (experiment builds): the hash waves' s_setprio level
+#ifndef NKFS_WS_HPRIO
+#define NKFS_WS_HPRIO 0
+#endif
 template <int K, int E, int NE, bool SB, int PF, int HW>
 __global__ __launch_bounds__(64 * (NE + HW)) void k_encode_ws(nkfs_geom g, const u8 *ids, u64 *digests, bool nt)
 {
@@ -219,6 +223,8 @@ __global__ __launch_bounds__(64 * (NE + HW)) void k_encode_ws(nkfs_geom g, const
     }
 
     // ------------------------------------------------------------ hash wave
+    if (NKFS_WS_HPRIO)
+        __builtin_amdgcn_s_setprio(NKFS_WS_HPRIO);
     constexpr int LPS = 64 / SPH;  // hash lanes per stripe (4 x E)
     const int hs = (wave - NE) * SPH + lane / LPS, hli = lane % LPS;
     const int hi = hli >> 2, ha = hli & 3;

@@ -65,6 +65,10 @@ struct RingStripe {
 // K: data parts; E: packed table bytes (4: n <= 4, 8: n <= 8); HW: hash waves;
 // PF: chunks of block loads in flight per encoder wave; RAGGED / DYN: ragged
 // geometry / device-wide group counter.
+// NKFS_WS_HPRIO (experiment builds): the hash waves' s_setprio level
+#ifndef NKFS_WS_HPRIO
+#define NKFS_WS_HPRIO 0
+#endif
 template <int K, int E, int HW, int PF, bool RAGGED, bool DYN>
 __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs_geom g, const u8 *ids,
                                                                             u64 *digests, u32 ngroups, bool nt)
@@ -480,6 +484,8 @@ __global__ __launch_bounds__(64 * (HW * 16 / E + HW + 1)) void k_encode_wsp(nkfs
     }
 
     // ------------------------------------------------------------ hash wave
+    if (NKFS_WS_HPRIO)
+        __builtin_amdgcn_s_setprio(NKFS_WS_HPRIO);
     constexpr int LPS = 64 / SPH;  // hash lanes per stripe (4 x E)
     const int hs = (wave - S) * SPH + lane / LPS, hli = lane % LPS;
     const int hi = hli >> 2, ha = hli & 3;
