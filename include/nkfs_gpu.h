@@ -107,19 +107,21 @@ struct nkfs_tune {
 	                         automatic choice is the walk encoder (ragged batches: 1, the default) or also the
 	                         warp-specialised grid (uniform batches: 2); 0 = off */
 	int dec_bign;         /* k > 8 decode on the stage-free decoder (nk8_bign.hip): -2 = auto (NKFS_DEC_AUTO only:
-	                         byte tables for k % 4 == 0 except 16, layout 3 for the other 16 < k <= 64),
+	                         diagonal byte tables (4) for k % 4 == 0 except 16, layout 3 for the other 16 < k <= 64),
 	                         -1 = off (survivor-table / column-chunked
 	                         decoders), 0 = byte tables, 1 = nibble tables x 16 replicas (every
 	                         lookup in its lane's own bank slot) in 16-survivor chunks, 2 = the same in 8-survivor
 	                         chunks (two workgroups per CU), 3 = every output column of a slice in one workgroup
-                         (8 < k <= 64; rows through an LDS stage, so odd k store whole 16-byte pieces) */
+                         (8 < k <= 64; rows through an LDS stage, so odd k store whole 16-byte pieces),
+	                         4 = byte tables in the diagonal layout (entry x of survivor j at x * 256 + j * 16, lane l
+	                         walking the survivors from l & 15: every lookup of a lane group in its own bank slot) */
 	int enc_bign;         /* k <= 76 encode on the stage-free encoder with a hash wave (nk8_bign.hip; units of 16
 	                         parts up to k = 32, of 8 parts above): -1 = auto
 	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64
 	                         pass), 1 = every k <= 76 batch it accepts, persistent (a workgroup per CU walking
-	                         the (stripe, part group) units), 2 = the same, one workgroup per unit, 3 = the
-	                         VALU encoder for every k (nk8_vp.hip: products by v_perm from 2-bit tables in scalar
-	                         registers, no LDS tables) */
+	                         the (stripe, part group) units), 2 = the same, one workgroup per unit, 3 = persistent
+	                         with diagonal (bank-conflict-free) tables for every 16 < k <= 32 (automatic for
+	                         k = 32) */
 	int dec_pair_pipe;    /* k = 2 decode of uniform batches of blocks <= 4 KiB (C2): waves per CU of the persistent
 	                         pipelined pair decoder (next stripes' slots, ids and parts in flight under the current
 	                         one), taken automatically when > 0; 0 = the wave decoder */

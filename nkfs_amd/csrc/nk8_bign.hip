@@ -116,7 +116,13 @@ __global__ __launch_bounds__(64 * BnShape<MODE>::WAVES, BnShape<MODE>::PER_CU) v
 {
     using SH = BnShape<MODE>;
     constexpr int CW = SH::CW, WAVES = SH::WAVES, T = SH::T, NT = 64 * WAVES;
-    constexpr bool NIB = MODE != 0;
+    constexpr bool NIB = MODE == 1 || MODE == 2;
+    // MODE 4: byte tables in the diagonal layout -- entry x of survivor j at
+    // x * 256 + j * 16, the chunk's 16 tables in the 16 bank slots of each x
+    // row -- and lane l walks the survivors from (l & 15): the 16 lanes of a
+    // b128 lane group read 16 distinct slots (MODE 0: random slots, ~3
+    // passes per group)
+    constexpr bool DIAG = MODE == 4;
     __shared__ __attribute__((aligned(16))) u8 tbl[SH::TBYTES];
     __shared__ __attribute__((aligned(16))) u32 wq[CW][4];  // a chunk's W rows, columns 16h ..
     __shared__ u32 wslot[CW];                               // a chunk's survivor slots
@@ -139,6 +145,16 @@ __global__ __launch_bounds__(64 * BnShape<MODE>::WAVES, BnShape<MODE>::PER_CU) v
     // H tables 64 KiB up through byte 2 of the high lookups' slot word
     const u32 slot_lo = NIB ? u32(lane & 15) * 16u : 0u;
     const u32 slot_hi = slot_lo | (MODE == 1 ? 0x10000u : 0u);
+    // DIAG: byte i of dslot[g] = the slot ((4 g + i + (lane & 15)) & 15) * 16
+    u32 dslot[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+        u32 x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            x |= (((u32(4 * gq + i) + u32(lane & 15)) & 15u) << 4) << (8 * i);
+        dslot[gq] = x;
+    }
 
     uint4 acc[T][4];
 
@@ -258,6 +274,38 @@ __global__ __launch_bounds__(64 * BnShape<MODE>::WAVES, BnShape<MODE>::PER_CU) v
                         make_uint4(e4[0], e4[1], e4[2], e4[3]);
                 }
             }
+        } else if constexpr (DIAG) {
+            // lane l builds table j = l & 15, entries x = (l >> 4) + 4 i + 32
+            // wave (Gray-code walk over i < 8): the 8 lanes of a ds_write_b128
+            // group write 8 slots of one x row (no conflict)
+            static_assert(WAVES == 8 && CW == 16, "diagonal build: 8 waves x 32 entries per table");
+            const int j = lane & 15, xl = lane >> 4;
+            const u32 row[4] = {wq[j][0], wq[j][1], wq[j][2], wq[j][3]};
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            u32 hv[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                u32 e = 0;
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb)
+                    e ^= basis[bb][w] & (0u - ((u32(xl) >> bb) & 1u));
+#pragma unroll
+                for (int bb = 0; bb < 3; ++bb)
+                    e ^= basis[5 + bb][w] & (0u - ((u32(wave) >> bb) & 1u));
+                hv[w] = e;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i) {
+                    const int bit = __builtin_ctz(i);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        hv[w] ^= basis[2 + bit][w];
+                }
+                const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 32u * u32(wave);
+                *reinterpret_cast<uint4 *>(tbl + x * 256u + u32(j) * 16u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            }
         } else {
             // byte tables: column j, entries x = lane + 64 m (Gray-code walk
             // over the two high bits, one XOR per entry)
@@ -316,6 +364,43 @@ __global__ __launch_bounds__(64 * BnShape<MODE>::WAVES, BnShape<MODE>::PER_CU) v
                         a4[q].w = xor3(a4[q].w, a.w, c2.w);
                     }
                     if (j & 1)
+                        asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
+                }
+            } else if constexpr (DIAG) {
+                // dd[t] = d[(t + r) & 15]: four mux stages by the bits of r
+                u32 dd[CW];
+#pragma unroll
+                for (int t = 0; t < CW; ++t)
+                    dd[t] = d[t];
+#pragma unroll
+                for (int st2 = 3; st2 >= 0; --st2) {
+                    const u32 mk = (u32(lane) >> st2) & 1u ? ~0u : 0u;
+                    u32 nx[CW];
+#pragma unroll
+                    for (int t = 0; t < CW; ++t)
+                        nx[t] = mux3(mk, dd[(t + (1 << st2)) & 15], dd[t]);
+#pragma unroll
+                    for (int t = 0; t < CW; ++t)
+                        dd[t] = nx[t];
+                }
+                // every step (survivors past k meet zero tables)
+#pragma unroll
+                for (int t = 0; t < CW; t += 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        // byte 0: the slot of survivor (t + r) & 15, byte 1: row q's byte
+                        const u32 s0 = 0x0C0C0004u | (u32(q) << 8) | u32(t & 3);
+                        const u32 s1 = 0x0C0C0004u | (u32(q) << 8) | u32((t + 1) & 3);
+                        const u32 P0 = __builtin_amdgcn_perm(dslot[t >> 2], dd[t], s0) + tdep;
+                        const u32 P1 = __builtin_amdgcn_perm(dslot[(t + 1) >> 2], dd[t + 1], s1) + tdep;
+                        const uint4 a = *reinterpret_cast<const uint4 *>(tbl + P0);
+                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + P1);
+                        a4[q].x = xor3(a4[q].x, a.x, c2.x);
+                        a4[q].y = xor3(a4[q].y, a.y, c2.y);
+                        a4[q].z = xor3(a4[q].z, a.z, c2.z);
+                        a4[q].w = xor3(a4[q].w, a.w, c2.w);
+                    }
+                    if (t & 2)
                         asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
                 }
             } else {
@@ -841,15 +926,18 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #ifndef NKFS_BE_PROG
 #define NKFS_BE_PROG 0
 #endif
-// NKFS_BE_HPRIO (experiment builds): the hash wave's s_setprio level (its
-// XXH64 chain is latency-bound and shares each SIMD with busy encoder waves)
-// NKFS_BE_HW (experiment builds): hash waves per workgroup (1, or 2 taking
-// alternate units)
+// NKFS_BE_HW: hash waves per workgroup, taking units in turn (default 4:
+// the XXH64 chains, not the encoders, bounded the fused kernel --
+// W2 1,703 -> 1,902, N24K20 1,665 -> 2,143, N20K17 1,382 -> 1,892 GB/s
+// with NKFS_BE_HPRIO 3; 6 and 8 lose again: profiles/r06/ab_bign_hwn.txt)
 #ifndef NKFS_BE_HW
-#define NKFS_BE_HW 1
+#define NKFS_BE_HW 4
 #endif
+// NKFS_BE_HPRIO: the hash waves' s_setprio level (default 3: an XXH64 chain
+// is latency-bound and shares its SIMD with busy encoder waves; W2 1,704 ->
+// 1,941 GB/s with one hash wave, profiles/r06/ab_bign_hprio.txt)
 #ifndef NKFS_BE_HPRIO
-#define NKFS_BE_HPRIO 0
+#define NKFS_BE_HPRIO 3
 #endif
 constexpr u32 BE_END = 0xFFFFFFFFu;
 
@@ -894,12 +982,16 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 {
     static_assert(P == 16 || (P == 8 && KC == 0), "part groups of 16, or of 8 without contiguous-row loads");
     static_assert(!DIAG || P == 16, "diagonal tables: units of 16 parts");
-    // HWV hash waves (1 or 2: units alternate between them), EW encoders
-    static_assert(HWV == 1 || HWV == 2, "one or two hash waves");
+    // HWV hash waves (units go round them), EW encoders
+    static_assert(HWV >= 1 && HWV <= 8, "one to eight hash waves");
     constexpr int EW = BE_WAVES - HWV;
-    constexpr u32 ROWS = 64u * EW * 4u;  // rows per slice (3,840 or 3,584: 120 or 112 XXH64 rounds)
+    constexpr u32 ROWS = 64u * EW * 4u;  // rows per slice (3,840 with one hash wave: 120 XXH64 rounds)
     constexpr u32 TB = BeShape<P>::TB;
     constexpr int TPW = 64 / P;  // tables whose Vandermonde row one wave computes per pass
+    // table passes per encoder wave: columns wave, wave + EW, ... must cover
+    // every column (P = 16: 32; P = 8: 76), at most TPW per wave
+    constexpr int TP = (BeShape<P>::CMAX + EW - 1) / EW;
+    static_assert(TP <= TPW, "too few encoder waves to build every column's table");
     __shared__ __attribute__((aligned(16))) u8 tbl[BeShape<P>::CMAX * TB];
     __shared__ __attribute__((aligned(16))) u8 vrow[DIAG ? 2 * 16 * 16 : 16];  // DIAG: the Vandermonde rows
     __shared__ u32 done[BE_WAVES];  // slices stored so far, per encoder wave
@@ -979,7 +1071,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             {
                 const int t = lane / P, e = lane % P, m = wave + EW * t;
                 u32 r = 0;
-                if (e < np && m < k && (P == 8 || t < 3)) {
+                if (e < np && m < k && t < TP) {
                     u32 x = ids[u64(s) * u64(n) + u64(p0 + e)];
                     r = 1;
 #pragma unroll
@@ -1001,7 +1093,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 // one x row (no conflict)
                 {
                     const int t = lane / 16, e = lane % 16, m = wave + EW * t;
-                    if (t < 3 && m < 16 * nch)
+                    if (t < TP && m < 16 * nch)
                         vrow[m * 16 + e] = u8(xb);
                 }
                 enc_barrier<EW>(&bar, gen, lane);
@@ -1031,7 +1123,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 }
             }
 #pragma unroll 1
-            for (int t = 0; t < (DIAG ? 0 : P == 16 ? 3 : TPW); ++t) {
+            for (int t = 0; t < (DIAG ? 0 : TP); ++t) {
                 const int m = wave + EW * t;
                 // P = 16: columns k .. 16 nch - 1 get zero tables (lookups in
                 // column pairs); P = 8: only columns < k exist -- 16 nch
@@ -1458,7 +1550,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const Stripe v = stripe_at(g, s);
             const int p0 = int(grp) * P, np = min(P, n - p0);  // P = 8: lanes 32.. idle (their e >= np)
             const u32 nsl = (v.ps + ROWS - 1) / ROWS;
-            if (HWV == 2 && int(ci & 1u) != wave - EW) {
+            if (HWV > 1 && int(ci % u32(HWV)) != wave - EW) {
                 seq += nsl;  // the other hash wave's unit
                 continue;
             }
@@ -1558,7 +1650,7 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
                                 hipStream_t st)
 {
     const int k = g->k;
-    if (k < 2 || k > 254 || mode < 0 || mode > 3 || (mode == 3 && (k <= 8 || k > 64)))
+    if (k < 2 || k > 254 || mode < 0 || mode > 4 || (mode == 3 && (k <= 8 || k > 64)))
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
@@ -1572,6 +1664,7 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
     case 0: return launch_bign<0>(g, work, status, pal, st);
     case 1: return launch_bign<1>(g, work, status, pal, st);
     case 2: return launch_bign<2>(g, work, status, pal, st);
+    case 4: return launch_bign<4>(g, work, status, pal, st);
     default:
         switch ((k + 15) / 16) {
         case 1: return launch_bigr<1, 1>(g, work, status, pal, st);
@@ -1628,7 +1721,7 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
         }
     }
     auto go = [&](auto hash, auto kcon) {
-        if (diag)
+        if (diag || k == 32)
             hipLaunchKernelGGL((k_encode_bign<16, decltype(hash)::value, decltype(kcon)::value, true, NKFS_BE_HW>), dim3(grid),
                                dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
         else

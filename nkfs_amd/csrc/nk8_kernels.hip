@@ -673,7 +673,6 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
                                 hipStream_t st);
 extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, bool persist,
                                 bool diag, hipStream_t st);
-extern "C" int nkfs_vp_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t *digests, hipStream_t st);
 extern "C" int nkfs_wide_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int cus,
                                 hipStream_t st);
 extern "C" int nkfs_slice_decode(const nkfs_geom *g, int n_slots, const u8 *ids, const u8 *avail, int navail,
@@ -803,20 +802,12 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
     // pinned with enc_bign 1) lose to the column-chunked encoder + hash
     // pass: W3 723 / 887, N40K33 762 / 977 GB/s (profiles/r06/ab_bign8_enc.txt)
     const int eb = nkfs_tune_now().enc_bign;
-    // enc_bign 3: the VALU encoder (nk8_vp.hip: products by v_perm from
-    // 2-bit tables in scalar registers, no LDS tables), any k
-    if (kern != NKFS_ENC_GENERIC && eb == 3) {
-        rc = nkfs_vp_encode(g, ids, digests, st);
+    if (kern != NKFS_ENC_GENERIC &&
+        (eb > 0 || (eb == -1 && digests && g->k > 16 && g->k <= 32 && kern == NKFS_ENC_AUTO))) {
+        // diagonal tables for k = 32, or every k with enc_bign 3
+        rc = nkfs_bign_encode(g, ids, digests, eb != 2, eb == 3, st);
         if (rc != -ENOSYS)
             return rc;
-    }
-    if (kern != NKFS_ENC_GENERIC && eb != 3 &&
-        (eb > 0 || (eb == -1 && digests && g->k > 16 && g->k <= 32 && kern == NKFS_ENC_AUTO))) {
-        // enc_bign 5 (experiment): diagonal tables without the hash wave,
-        // then the batched XXH64 pass over the parts
-        rc = nkfs_bign_encode(g, ids, eb == 5 ? nullptr : digests, eb != 2, eb >= 4, st);
-        if (rc != -ENOSYS)
-            return rc || eb != 5 || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
     }
     // n > 8 (or a few big stripes), k <= 16: with digests and a batch that
     // fills the chip (two workgroups of 16 parts per CU), the part-group
@@ -955,12 +946,16 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     // W3 N64K41 491 -> 875 GB/s (profiles/r06/ab_bigr_*.txt); k % 4 == 0 keeps
     // the byte-table form (W2 2,064 vs 1,341).  The automatic choice applies
     // to NKFS_DEC_AUTO only: a pinned NKFS_DEC_BIG runs the column-chunked
-    // decoder unless dec_bign pins a stage-free layout
+    // decoder unless dec_bign pins a stage-free layout.
+    // Round 6 (later): the byte tables in the diagonal layout (dec_bign 4:
+    // conflict-free lookups) replace layout 0 in the automatic choice -- W2
+    // 2,068 -> 2,680 GB/s, N24K20 1,116 -> 1,180, N32K28 608 -> 639, W1
+    // 4,292 -> 4,301 (profiles/r06/ab_diag_dec.txt)
     rc = -ENOSYS;
     if (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG) {
         int mode = t.dec_bign;
         if (mode == -2 && t.dec_kernel == NKFS_DEC_AUTO)
-            mode = g->k % 4 == 0 && g->k != 16 ? 0 : g->k > 16 && g->k <= 64 ? 3 : -1;
+            mode = g->k % 4 == 0 && g->k != 16 ? 4 : g->k > 16 && g->k <= 64 ? 3 : -1;
         if (mode >= 0)
             rc = nkfs_bign_decode(g, (const u8 *)work, status, mode, st);
     }

@@ -84,9 +84,12 @@ def test_big_encode_matches(L, O, n, k, B, S):
     with _tuned(enc_kernel=_lib.ENC["big"], enc_big_fused=1):  # XXH64 fused, chained over the slices
         p3, d3 = batch.encode(blocks, B, n, k, ids)
     p2, d2 = batch.encode(blocks, B, n, k, ids)  # default dispatch
-    with _tuned(enc_bign=1):  # the stage-free encoder, hash wave and no-digest forms
+    with _tuned(enc_bign=1):  # the stage-free encoder, hash waves and no-digest forms
         p4, d4 = batch.encode(blocks, B, n, k, ids)
         p5, _ = batch.encode(blocks, B, n, k, ids, digests=False)
+    with _tuned(enc_bign=3):  # diagonal (bank-conflict-free) tables at every 16 < k <= 32
+        p6, d6 = batch.encode(blocks, B, n, k, ids)
+        p7, _ = batch.encode(blocks, B, n, k, ids, digests=False)
     torch.cuda.synchronize()
     ps = batch.part_size(B, k)
     assert torch.equal(p0[:, :ps], p1[:, :ps]) and torch.equal(d0, d1)
@@ -94,6 +97,8 @@ def test_big_encode_matches(L, O, n, k, B, S):
     assert torch.equal(p0[:, :ps], p2[:, :ps]) and torch.equal(d0, d2)
     assert torch.equal(p0[:, :ps], p4[:, :ps]) and torch.equal(d0, d4)
     assert torch.equal(p0[:, :ps], p5[:, :ps])
+    assert torch.equal(p0[:, :ps], p6[:, :ps]) and torch.equal(d0, d6)
+    assert torch.equal(p0[:, :ps], p7[:, :ps])
     got = [u64(x) for x in d1.cpu().tolist()]
     for s in sorted({0, S - 1}):
         want = O.encode(blocks[s, :B].cpu().numpy(), n, k, ids_np[s])
@@ -121,7 +126,7 @@ def test_big_encode_ragged(L, O, n, k, gap):
     ids_np = synth.batch_ids(len(sizes), n, first=500)
     outs = []
     for kern, fused, eb in (("generic", 0, 0), ("big", 0, 0), ("big", 1, 0), ("auto", 0, -1), ("auto", 0, 1),
-                            ("auto", -1, -1)):
+                            ("auto", -1, -1), ("auto", 0, 3)):
         parts = torch.zeros(ppos, dtype=torch.uint8, device="cuda")
         dig = torch.zeros(len(sizes) * n, dtype=torch.int64, device="cuda")
         with _tuned(enc_kernel=_lib.ENC[kern], enc_big_fused=fused, enc_bign=eb):
@@ -177,7 +182,7 @@ def test_big_decode_matches(L, O, n, k, B, S):
     # the column-chunked decoder, then the replicated-table decoder
     # (nk8_bign.hip) in its three table layouts
     for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2),
-                       ("auto", -2), ("big", 3), ("auto", 3)):
+                       ("auto", -2), ("big", 3), ("auto", 3), ("big", 4), ("auto", 4)):
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
@@ -271,7 +276,7 @@ def test_big_round_trip_w2(L, O):
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     assert torch.equal(out, blocks[:, :B])
-    for mode in (-1, 0, 1, 2, 3):  # the survivor-table decoder, the stage-free one's layouts
+    for mode in (-1, 0, 1, 2, 3, 4):  # the survivor-table decoder, the stage-free one's layouts
         with _tuned(dec_bign=mode):
             out2, status2 = batch.decode(parts, n, ids, avail, k, B)
         torch.cuda.synchronize()

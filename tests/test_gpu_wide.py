@@ -177,7 +177,7 @@ def test_wide_decode_matches(L, O, n, k, B, S):
         ids2[2, :] = ids2[2, 0]
     outs = []
     for kern, mode in (("generic", -1), ("wide", -1), ("auto", -1), ("auto", 0), ("auto", 1), ("auto", 2),
-                       ("auto", -2)):
+                       ("auto", -2), ("auto", 4)):
         from nkfs_amd import _lib
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
