@@ -107,14 +107,15 @@ struct nkfs_tune {
 	                         automatic choice is the walk encoder (ragged batches: 1, the default) or also the
 	                         warp-specialised grid (uniform batches: 2); 0 = off */
 	int dec_bign;         /* k > 8 decode on the stage-free decoder (nk8_bign.hip): -2 = auto (NKFS_DEC_AUTO only:
-	                         diagonal byte tables (4) for k % 4 == 0 except 16, layout 3 for the other 16 < k <= 64),
+	                         diagonal byte tables (4) for k % 4 == 0 except 16, layout 5 for the other 16 < k <= 64),
 	                         -1 = off (survivor-table / column-chunked
 	                         decoders), 0 = byte tables, 1 = nibble tables x 16 replicas (every
 	                         lookup in its lane's own bank slot) in 16-survivor chunks, 2 = the same in 8-survivor
 	                         chunks (two workgroups per CU), 3 = every output column of a slice in one workgroup
                          (8 < k <= 64; rows through an LDS stage, so odd k store whole 16-byte pieces),
 	                         4 = byte tables in the diagonal layout (entry x of survivor j at x * 256 + j * 16, lane l
-	                         walking the survivors from l & 15: every lookup of a lane group in its own bank slot) */
+	                         walking the survivors from l & 15: every lookup of a lane group in its own bank slot),
+	                         5 = layout 3 with diagonal tables (k <= 48; beyond, layout 3) */
 	int enc_bign;         /* k <= 76 encode on the stage-free encoder with a hash wave (nk8_bign.hip; units of 16
 	                         parts up to k = 32, of 8 parts above): -1 = auto
 	                         (16 < k <= 32 with digests, persistent), 0 = off (column-chunked encoder + XXH64

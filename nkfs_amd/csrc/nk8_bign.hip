@@ -593,10 +593,15 @@ struct BrShape {
 #ifndef BR_WPE
 #define BR_WPE 4
 #endif
-template <int NG, int T, bool PAL>
+// DIAG (dec_bign 5, NG <= 3): a (chunk, group)'s 16 tables in the diagonal
+// layout of k_decode_bign MODE 4 (entry x of survivor j at x * 256 + j * 16),
+// the survivor dwords rotated once per chunk by l & 15 and shared by the NG
+// groups: every lookup of a b128 lane group in its own bank slot
+template <int NG, int T, bool PAL, bool DIAG>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_WPE))) void k_decode_bigr(nkfs_geom g, const u8 *work, const int32_t *status,
                                                          u32 nslices, u32 nwg)
 {
+    static_assert(!DIAG || NG <= 3, "diagonal tables: branch-free survivor loads (NG <= 3)");
     using SH = BrShape<NG, T>;
     constexpr int CW = SH::CW, NT = SH::NT, KP = SH::KMAX;
     __shared__ __attribute__((aligned(16))) u8 tbl[CW * 4096];  // tables; the output stage after the lookups
@@ -715,6 +720,90 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
             build_table16(tbl + u32(j) * 4096u, basis, lane);
         }
     };
+    // DIAG: lane l builds table j = l & 15 of the (chunk, group), entries x =
+    // (l >> 4) + 4 i + 32 wave (Gray-code walk over i < 8; the 8 lanes of a
+    // ds_write_b128 group write 8 slots of one x row); rows past k are zero
+    auto build_diag = [&](int cc, int h) {
+        const int j = lane & 15, xl = lane >> 4;
+        const uint4 r4 = *reinterpret_cast<const uint4 *>(wl + (CW * cc + j) * KP + 16 * h);
+        const u32 row[4] = {r4.x, r4.y, r4.z, r4.w};
+        u32 basis[8][4];
+        make_basis<4>(basis, row);
+        u32 hv[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            u32 e = 0;
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+                e ^= basis[bb][w] & (0u - ((u32(xl) >> bb) & 1u));
+#pragma unroll
+            for (int bb = 0; bb < 3; ++bb)
+                e ^= basis[5 + bb][w] & (0u - ((u32(wave) >> bb) & 1u));
+            hv[w] = e;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i) {
+                const int bit = __builtin_ctz(i);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    hv[w] ^= basis[2 + bit][w];
+            }
+            const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 32u * u32(wave);
+            *reinterpret_cast<uint4 *>(tbl + x * 256u + u32(j) * 16u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+        }
+    };
+    // DIAG: byte i of dslot[gq] = the slot ((4 gq + i + (lane & 15)) & 15) * 16
+    u32 dslot[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+        u32 x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            x |= (((u32(4 * gq + i) + u32(lane & 15)) & 15u) << 4) << (8 * i);
+        dslot[gq] = x;
+    }
+    // DIAG: dd[t] = d[(t + (l & 15)) & 15], four mux stages
+    auto rotate = [&](const u32 (&d)[CW], u32 (&dd)[CW]) {
+#pragma unroll
+        for (int t = 0; t < CW; ++t)
+            dd[t] = d[t];
+#pragma unroll
+        for (int st2 = 3; st2 >= 0; --st2) {
+            const u32 mk = (u32(lane) >> st2) & 1u ? ~0u : 0u;
+            u32 nx[CW];
+#pragma unroll
+            for (int t = 0; t < CW; ++t)
+                nx[t] = mux3(mk, dd[(t + (1 << st2)) & 15], dd[t]);
+#pragma unroll
+            for (int t = 0; t < CW; ++t)
+                dd[t] = nx[t];
+        }
+    };
+    auto quad_diag = [&](const u32 (&dd)[CW], uint4 (&a4)[4]) {
+        u32 tdep;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(tdep));
+#pragma unroll
+        for (int j = 0; j < CW; j += 2) {
+            const u32 dj0 = dd[j] ^ tdep, dj1 = dd[j + 1] ^ tdep;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // byte 0: the slot of survivor (j + r) & 15, byte 1: row q's byte
+                const u32 s0 = 0x0C0C0004u | (u32(q) << 8) | u32(j & 3);
+                const u32 s1 = 0x0C0C0004u | (u32(q) << 8) | u32((j + 1) & 3);
+                const u32 P0 = __builtin_amdgcn_perm(dslot[j >> 2], dj0, s0);
+                const u32 P1 = __builtin_amdgcn_perm(dslot[(j + 1) >> 2], dj1, s1);
+                const uint4 a = *reinterpret_cast<const uint4 *>(tbl + P0);
+                const uint4 c2 = *reinterpret_cast<const uint4 *>(tbl + P1);
+                a4[q].x = xor3(a4[q].x, a.x, c2.x);
+                a4[q].y = xor3(a4[q].y, a.y, c2.y);
+                a4[q].z = xor3(a4[q].z, a.z, c2.z);
+                a4[q].w = xor3(a4[q].w, a.w, c2.w);
+            }
+            if ((j & (BR_PAIRS * 2 - 2)) == BR_PAIRS * 2 - 2)
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(a4[3].x));
+        }
+    };
 
     u8 *out = const_cast<u8 *>(v.blk);
     const bool oal = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
@@ -759,6 +848,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
 #pragma unroll
                 for (int t = 0; t < T; ++t)
                     load(d[(cc + 1) & 1][t], r_begin + (u32(t) * u32(NT) + u32(tid)) * 4u, cc + 1);
+            if constexpr (DIAG) {
+                u32 dd[T][CW];
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    rotate(d[cc & 1][t], dd[t]);
+#pragma unroll
+                for (int h = 0; h < NG; ++h) {
+                    lds_barrier();  // the previous tables' lookups (or stage reads) are done
+                    build_diag(cc, h);
+                    lds_barrier();
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+                        quad_diag(dd[t], acc[t][h]);
+                }
+            } else {
 #pragma unroll
             for (int h = 0; h < NG; ++h) {
                 lds_barrier();  // the previous tables' lookups (or stage reads) are done
@@ -767,6 +871,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
 #pragma unroll
                 for (int t = 0; t < T; ++t)
                     quad(d[cc & 1][t], acc[t][h], cc);
+            }
             }
         }
         lds_barrier();  // every lookup is done: the table LDS becomes the stage
@@ -834,7 +939,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BR_WPE, BR_
     }
 }
 
-template <int NG, int T>
+template <int NG, int T, bool DIAG>
 int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, bool pal, hipStream_t st)
 {
     using SH = BrShape<NG, T>;
@@ -854,9 +959,9 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
     if (u64(g->n) * pitch_max >= 0xFFFFFFFFull)
         return -ENOSYS;
     if (pal)
-        hipLaunchKernelGGL((k_decode_bigr<NG, T, true>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
+        hipLaunchKernelGGL((k_decode_bigr<NG, T, true, DIAG>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
     else
-        hipLaunchKernelGGL((k_decode_bigr<NG, T, false>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
+        hipLaunchKernelGGL((k_decode_bigr<NG, T, false, DIAG>), dim3(u32(grid)), dim3(SH::NT), 0, st, *g, work, status, ns, nwg);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -932,6 +1037,11 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 // with NKFS_BE_HPRIO 3; 6 and 8 lose again: profiles/r06/ab_bign_hwn.txt)
 #ifndef NKFS_BE_HW
 #define NKFS_BE_HW 4
+#endif
+// NKFS_BE_RING: the hash waves' load ring, in batches of 8 rounds (RING - 1
+// batches in flight while one is folded)
+#ifndef NKFS_BE_RING
+#define NKFS_BE_RING 4
 #endif
 // NKFS_BE_HPRIO: the hash waves' s_setprio level (default 3: an XXH64 chain
 // is latency-bound and shares its SIMD with busy encoder waves; W2 1,704 ->
@@ -1602,20 +1712,18 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                         w[i] = (u64(x.y) << 32) | x.x;
                     }
                 };
-                uint64_t w0[8], w1[8], w2[8], w3[8];
-                ld(w0, rb);
-                ld(w1, rb + 8);
-                ld(w2, rb + 16);
+                constexpr int RB = NKFS_BE_RING;  // batches of 8 rounds, RB - 1 in flight
+                uint64_t w[RB][8];
+#pragma unroll
+                for (int i = 0; i < RB - 1; ++i)
+                    ld(w[i], rb + 8u * u32(i));
 #pragma unroll 1
-                for (int r = int(rb); r < re; r += 32) {
-                    ld(w3, u32(r) + 24);
-                    hacc = xxh_rounds<8>(hacc, w0, re - r);
-                    ld(w0, u32(r) + 32);
-                    hacc = xxh_rounds<8>(hacc, w1, re - r - 8);
-                    ld(w1, u32(r) + 40);
-                    hacc = xxh_rounds<8>(hacc, w2, re - r - 16);
-                    ld(w2, u32(r) + 48);
-                    hacc = xxh_rounds<8>(hacc, w3, re - r - 24);
+                for (int r = int(rb); r < re; r += 8 * RB) {
+#pragma unroll
+                    for (int i = 0; i < RB; ++i) {
+                        ld(w[(i + RB - 1) % RB], u32(r) + 8u * u32(i + RB - 1));
+                        hacc = xxh_rounds<8>(hacc, w[i], re - r - 8 * i);
+                    }
                 }
             }
             // every slice is stored: the tail (ps & 31 bytes after the last
@@ -1645,12 +1753,14 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 // Decode a uniform or ragged batch with 2 <= k <= 254 from the plan
 // k_decode_prep left in `work` (stripes with status != 0 are skipped), with
 // table layout `mode` (0 byte tables, 1 nibble x 16 replicas in 16-survivor
-// chunks, 2 nibble x 16 replicas in 8-survivor chunks).
+// chunks, 2 nibble x 16 replicas in 8-survivor chunks, 3 every output column
+// of a slice in one workgroup, 4 byte tables in the diagonal layout, 5 = 3
+// with diagonal tables).
 extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const int32_t *status, int mode,
                                 hipStream_t st)
 {
     const int k = g->k;
-    if (k < 2 || k > 254 || mode < 0 || mode > 4 || (mode == 3 && (k <= 8 || k > 64)))
+    if (k < 2 || k > 254 || mode < 0 || mode > 5 || ((mode == 3 || mode == 5) && (k <= 8 || k > 64)))
         return -ENOSYS;
     if (!g->nstripes)
         return 0;
@@ -1665,12 +1775,19 @@ extern "C" int nkfs_bign_decode(const nkfs_geom *g, const uint8_t *work, const i
     case 1: return launch_bign<1>(g, work, status, pal, st);
     case 2: return launch_bign<2>(g, work, status, pal, st);
     case 4: return launch_bign<4>(g, work, status, pal, st);
+    case 5:  // layout 3 with diagonal tables (NG <= 3; beyond, layout 3)
+        switch ((k + 15) / 16) {
+        case 1: return launch_bigr<1, 1, true>(g, work, status, pal, st);
+        case 2: return launch_bigr<2, 1, true>(g, work, status, pal, st);
+        case 3: return launch_bigr<3, 1, true>(g, work, status, pal, st);
+        default: return launch_bigr<4, 1, false>(g, work, status, pal, st);
+        }
     default:
         switch ((k + 15) / 16) {
-        case 1: return launch_bigr<1, 1>(g, work, status, pal, st);
-        case 2: return launch_bigr<2, 1>(g, work, status, pal, st);
-        case 3: return launch_bigr<3, 1>(g, work, status, pal, st);
-        default: return launch_bigr<4, 1>(g, work, status, pal, st);
+        case 1: return launch_bigr<1, 1, false>(g, work, status, pal, st);
+        case 2: return launch_bigr<2, 1, false>(g, work, status, pal, st);
+        case 3: return launch_bigr<3, 1, false>(g, work, status, pal, st);
+        default: return launch_bigr<4, 1, false>(g, work, status, pal, st);
         }
     }
 }

@@ -950,12 +950,15 @@ extern "C" int nkfs_launch_decode(const nkfs_geom *g, int n_slots, const uint8_t
     // Round 6 (later): the byte tables in the diagonal layout (dec_bign 4:
     // conflict-free lookups) replace layout 0 in the automatic choice -- W2
     // 2,068 -> 2,680 GB/s, N24K20 1,116 -> 1,180, N32K28 608 -> 639, W1
-    // 4,292 -> 4,301 (profiles/r06/ab_diag_dec.txt)
+    // 4,292 -> 4,301 (profiles/r06/ab_diag_dec.txt); the all-groups decoder
+    // with diagonal tables (dec_bign 5) replaces layout 3 -- W3 985 -> 1,489,
+    // N40K33 1,242 -> 1,636, N24K18 1,688 -> 1,895, N40K17 1,637 -> 1,784
+    // (profiles/r06/ab_bigr_diag.txt)
     rc = -ENOSYS;
     if (t.dec_kernel == NKFS_DEC_AUTO || t.dec_kernel == NKFS_DEC_BIG) {
         int mode = t.dec_bign;
         if (mode == -2 && t.dec_kernel == NKFS_DEC_AUTO)
-            mode = g->k % 4 == 0 && g->k != 16 ? 4 : g->k > 16 && g->k <= 64 ? 3 : -1;
+            mode = g->k % 4 == 0 && g->k != 16 ? 4 : g->k > 16 && g->k <= 64 ? 5 : -1;
         if (mode >= 0)
             rc = nkfs_bign_decode(g, (const u8 *)work, status, mode, st);
     }

@@ -103,7 +103,7 @@ int nkfs_tune_set(const struct nkfs_tune *t)
 	    (t->enc_ws_waves != 4 && t->enc_ws_waves != 6) || (t->dec_pair_waves != 1 && t->dec_pair_waves != 4) ||
 	    t->enc_few_max < 0 || t->enc_few_max > 63 || t->enc_ws_hash_waves < 0 || t->enc_ws_hash_waves > 2 ||
 	    t->enc_persist < 0 || t->enc_persist > 2 ||
-	    t->dec_bign < -2 || t->dec_bign > 4 || t->enc_bign < -1 || t->enc_bign > 3 ||
+	    t->dec_bign < -2 || t->dec_bign > 5 || t->enc_bign < -1 || t->enc_bign > 3 ||
 	    t->dec_pair_pipe < 0 || t->dec_pair_pipe > 32)
 		return -EINVAL;
 	pthread_mutex_lock(&g_tune_lock);

@@ -275,7 +275,7 @@ def test_tune_struct_and_ranges():
     assert (t0.enc_persist, t0.dec_bign, t0.enc_bign, t0.dec_pair_pipe) == (1, -2, -1, 0)
     L = _lib.lib()
     for field, bad, good in (("enc_bign", 4, 3), ("enc_bign", -2, 0), ("dec_pair_pipe", 33, 8),
-                             ("dec_pair_pipe", -1, 0), ("dec_bign", 5, 4), ("enc_persist", 3, 2)):
+                             ("dec_pair_pipe", -1, 0), ("dec_bign", 6, 5), ("enc_persist", 3, 2)):
         t = _lib.get_tune()
         setattr(t, field, bad)
         assert L.nkfs_tune_set(C.byref(t)) == -22, field

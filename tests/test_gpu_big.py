@@ -182,7 +182,7 @@ def test_big_decode_matches(L, O, n, k, B, S):
     # the column-chunked decoder, then the replicated-table decoder
     # (nk8_bign.hip) in its three table layouts
     for kern, mode in (("generic", -1), ("big", -1), ("auto", -1), ("big", 0), ("big", 1), ("big", 2), ("auto", 2),
-                       ("auto", -2), ("big", 3), ("auto", 3), ("big", 4), ("auto", 4)):
+                       ("auto", -2), ("big", 3), ("auto", 3), ("big", 4), ("auto", 4), ("auto", 5)):
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
             out = torch.full((S, B), 0xEE, dtype=torch.uint8, device="cuda")
             _, st = batch.decode(parts, n, dev(ids2), dev(av), k, B, out=out)
@@ -232,7 +232,7 @@ def test_bigr_decode_ragged(L, O, n, k, gap):
                         int(sizes.max()))
     av = synth.batch_survivors(len(sizes), n, k, first=800)
     outs = []
-    for kern, mode in (("generic", -1), ("big", -1), ("big", 3), ("auto", 3)):
+    for kern, mode in (("generic", -1), ("big", -1), ("big", 3), ("auto", 3), ("auto", 5)):
         out = torch.full((pos + 16,), 0xEE, dtype=torch.uint8, device="cuda")
         st = torch.full((len(sizes),), 5, dtype=torch.int32, device="cuda")
         with _tuned(dec_kernel=_lib.DEC[kern], dec_bign=mode):
@@ -276,7 +276,7 @@ def test_big_round_trip_w2(L, O):
     torch.cuda.synchronize()
     assert int(status.abs().sum()) == 0
     assert torch.equal(out, blocks[:, :B])
-    for mode in (-1, 0, 1, 2, 3, 4):  # the survivor-table decoder, the stage-free one's layouts
+    for mode in (-1, 0, 1, 2, 3, 4, 5):  # the survivor-table decoder, the stage-free one's layouts
         with _tuned(dec_bign=mode):
             out2, status2 = batch.decode(parts, n, ids, avail, k, B)
         torch.cuda.synchronize()
