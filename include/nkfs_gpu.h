@@ -92,7 +92,8 @@ struct nkfs_tune {
 	int enc_ws_prefetch;  /* warp-specialised encoders (n > 4, and the n > 8 fused part-group encoder): chunks of
 	                         loads in flight per encoder wave (1, 2; default 2) */
 	int enc_big_fused;    /* column-chunked k > 16 encoder: 1 = XXH64 fused (traffic 1.0x), 0 = second pass, -1 = auto
-	                         (default: fused for k > 32 -- W3 +4 %; 16 < k <= 32 with digests take the stage-free encoder) */
+	                         (default: the second pass -- W3 +10 % with the diagonal tables; 16 < k <= 32 with digests
+	                         take the stage-free encoder) */
 	int dec_pair_stage;   /* k = 2 decoder: 1 = output through an LDS stage (1 KiB runs per store), 0 = direct */
 	int host_depth;       /* host-memory entry points: sub-batches in flight per lane (2..8) */
 	int host_lanes;       /* host-memory entry points: host threads (lanes) per device (1..4) */

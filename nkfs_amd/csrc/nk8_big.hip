@@ -88,6 +88,24 @@ struct BigChain {
 // this wave's XCC (hardware register XCC_ID, bits 3:0)
 __device__ inline u32 xcc_id() { return u32(__builtin_amdgcn_s_getreg(20 | (3 << 11))) & 15u; }
 
+// NKFS_BIG_DIAG (default 1): k_encode_big's chunk tables in the diagonal
+// layout -- entry x of column j at x * 256 + j * 16, the 16 tables in the 16
+// bank slots of each x row -- and lane l walks a row's 16 columns from
+// (l & 15) (its bytes rotated by l & 15): the 16 lanes of every b128 lane
+// group read 16 distinct bank slots instead of random ones
+#ifndef NKFS_BIG_DIAG
+#define NKFS_BIG_DIAG 1
+#endif
+
+// a ^ b ^ c and mask ? a : b per bit, each one v_bitop3_b32 (operand truth
+// tables S0 0xF0, S1 0xCC, S2 0xAA)
+__device__ __forceinline__ u32 big_mux(u32 mask, u32 a, u32 b)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xE4" : "=v"(r) : "v"(a), "v"(b), "v"(mask));
+    return r;
+}
+
 constexpr u64 CHAIN_TIMEOUT = 200000;  // s_memrealtime ticks (100 MHz): 2 ms (a slice takes ~35 us)
 
 template <bool HASH>
@@ -157,10 +175,55 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
 #pragma unroll
     for (int t = 0; t < ENC_T; ++t)
         acc[t] = make_uint4(0, 0, 0, 0);
+    // NKFS_BIG_DIAG: this lane's rotation r = l & 15 and the slot bytes
+    // (byte i of dslot[gq] = ((4 gq + i + r) & 15) * 16)
+    const u32 r16 = u32(lane & 15);
+    const u32 mk8 = (r16 & 8u) ? ~0u : 0u, mk4 = (r16 & 4u) ? ~0u : 0u, rb3 = r16 & 3u;
+    u32 dslot[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+        u32 x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            x |= (((u32(4 * gq + i) + r16) & 15u) << 4) << (8 * i);
+        dslot[gq] = x;
+    }
 
     const int nch = (k + 15) / 16;
     for (int cc = 0; cc < nch; ++cc) {
         __syncthreads();  // coef[] written / the previous chunk's lookups done
+        if (NKFS_BIG_DIAG) {
+            // lane l builds table j = l & 15, entries x = (l >> 4) + 4 i + 64
+            // wave (Gray-code walk over i < 16): the 8 lanes of a
+            // ds_write_b128 group write 8 slots of one x row (no conflict)
+            const int j = lane & 15, xl = lane >> 4, m = 16 * cc + j;
+            const uint4 c = m < k ? coef[m] : make_uint4(0, 0, 0, 0);  // columns past k: zero table
+            const u32 row[4] = {c.x, c.y, c.z, c.w};
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            u32 hv[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                u32 e = 0;
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb) {
+                    e ^= basis[bb][w] & (0u - ((u32(xl) >> bb) & 1u));
+                    e ^= basis[6 + bb][w] & (0u - ((u32(wave) >> bb) & 1u));
+                }
+                hv[w] = e;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (i) {
+                    const int bit = __builtin_ctz(i);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        hv[w] ^= basis[2 + bit][w];
+                }
+                const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 64u * u32(wave);
+                *reinterpret_cast<uint4 *>(tbl + x * 256u + u32(j) * 16u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            }
+        } else {
         // wave w builds tables j = w, w+4, w+8, w+12 of columns 16cc + j
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
@@ -170,6 +233,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
             u32 basis[8][4];
             make_basis<4>(basis, row);
             build_table16(tbl + j * 4096, basis, lane);
+        }
         }
         __syncthreads();
         // tdep (0 at run time) chains each row's lookups and the next row's
@@ -216,6 +280,32 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                     }
                 }
                 uint4 e = acc[t];
+                if (NKFS_BIG_DIAG) {
+                    // the row's 16 bytes rotated by r = l & 15 (dword
+                    // rotation by two mux stages, byte rotation by
+                    // v_alignbyte); step j: column (j + r) & 15, address
+                    // x * 256 + its slot (dslot bytes)
+                    u32 a[4], b2[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        a[w] = big_mux(mk8, d[(w + 2) & 3], d[w]);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        b2[w] = big_mux(mk4, a[(w + 1) & 3], a[w]);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        d[w] = __builtin_amdgcn_alignbyte(b2[(w + 1) & 3], b2[w], rb3);
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const u32 sel = 0x0C0C0004u | (u32(j & 3) << 8) | u32(j & 3);
+                        const u32 P = __builtin_amdgcn_perm(dslot[j >> 2], d[j >> 2], sel) + tdep;
+                        const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + P);
+                        e.x ^= tv.x;
+                        e.y ^= tv.y;
+                        e.z ^= tv.z;
+                        e.w ^= tv.w;
+                    }
+                } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const u32 byte = (d[j >> 2] >> (8 * (j & 3))) & 0xFFu;
@@ -224,6 +314,7 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
                     e.y ^= tv.y;
                     e.z ^= tv.z;
                     e.w ^= tv.w;
+                }
                 }
                 acc[t] = e;
                 asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));

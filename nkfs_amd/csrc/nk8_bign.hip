@@ -1847,7 +1847,7 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     };
     auto pick = [&](auto hash) {
         if (P == 8) {
-            hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0, false, 1>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
+            hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0, false, NKFS_BE_HW>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
                                *g, ids, digests, u32(ngroups), u32(nunits), uctr);
             return;
         }

@@ -828,8 +828,12 @@ extern "C" int nkfs_launch_encode(const nkfs_geom *g, const uint8_t *ids, uint64
         rc = kern == NKFS_ENC_BIG ? -ENOSYS : nkfs_wide_encode(g, ids, nkfs_cu_count(), st);
         if (rc != -ENOSYS)
             return rc || !digests ? rc : nkfs_launch_hash_parts(g, digests, stream);
-        const int fz = nkfs_tune_now().enc_big_fused;  // -1 auto: fused for k > 32
-        rc = digests && (fz > 0 || (fz < 0 && g->k > 32)) ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
+        // -1 auto: the XXH64 pass (round 6, with the diagonal tables the
+        // slices' serial chain hand-off became the fused form's bound: W3
+        // 941 -> 1,039, N40K33 968 -> 1,078, N80K70 796 -> 866 GB/s,
+        // profiles/r06/ab_w3_enc.txt; it had won 880 -> 914 on W3 before)
+        const int fz = nkfs_tune_now().enc_big_fused;
+        rc = digests && fz > 0 ? nkfs_big_encode(g, ids, digests, gf, st) : -ENOSYS;
         if (rc != -ENOSYS)
             return rc;
         rc = nkfs_big_encode(g, ids, nullptr, gf, st);

@@ -71,7 +71,7 @@ static struct nkfs_tune g_tune = {
 	.dec_bign = -2, /* auto: byte tables for k % 4 == 0 (not 16), all-groups form for the other 16 < k <= 64
 	                 * (profiles/r05/ab_bign.txt, profiles/r06/ab_bigr_*.txt, ab_rule_k*.txt) */
 	.enc_bign = -1,
-	.enc_big_fused = -1, /* auto: XXH64 fused for k > 32 (W3 +4 %, HBM traffic 1.04x; profiles/r06/ab_w3_fused.txt) */
+	.enc_big_fused = -1, /* auto: the XXH64 pass (round 6: W3 +10 % over the fused chain with diagonal tables; profiles/r06/ab_w3_enc.txt) */
 	.dec_pair_pipe = 0,
 	.dec_pair_waves = 1, /* C2: 1 wave per workgroup 5,214 / 4 waves 5,116 GB/s (profiles/r04/ab_c2_pair4.txt) */
 };
