@@ -163,6 +163,16 @@ __device__ __forceinline__ void chain_run(const nkfs_xxh_args &a, u8 *ring, bool
         tw[w] = x;
     }
     const u64 dig = xxh_tail_regs(h, tw, a.tail_len);
+    if (!(a.flags & NKFS_XXH_EMIT) && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0) {
+        // digest and completion word in one 16-byte system-scope store:
+        // one posted write over the link, so the host that sees the word
+        // sees the digest (the NVMe completion-entry pattern) -- the
+        // two-store form waited for the digest's acknowledgement (a link
+        // round trip) before the word could leave
+        const v4u pk = {u32(dig), u32(dig >> 32), u32(a.flag), u32(a.flag >> 32)};
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(a.out), "v"(pk) : "memory");
+        return;
+    }
     put(a.out, dig);
     complete();  // the completion word after the digest, visible in order
 }
@@ -185,6 +195,9 @@ __global__ __launch_bounds__(64) void k_xxh64_chain(nkfs_xxh_args a)
 // The request half (seq, op, args, inline bytes) is read from `mb` -- host
 // memory, or (mode 2) fine-grained device memory the host writes over the
 // BAR -- and the answer half (taken, alive) written to `ob` in host memory.
+#ifndef NKFS_SVC_RELAXED_POLL
+#define NKFS_SVC_RELAXED_POLL 0
+#endif
 __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, nkfs_svc_box *ob, u64 idle, u64 life)
 {
     __shared__ __attribute__((aligned(16))) u8 ring[NS * 1024];
@@ -192,8 +205,14 @@ __global__ __launch_bounds__(64) void k_xxh64_service(nkfs_svc_box *mb, nkfs_svc
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
     u64 tl = t0;
     for (;;) {
-        const u64 sq = __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // NKFS_SVC_RELAXED_POLL (experiment builds): poll relaxed and acquire
+        // only once a request is seen
+        const u64 sq = NKFS_SVC_RELAXED_POLL
+                           ? __hip_atomic_load(&mb->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                           : __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (sq != last) {
+            if (NKFS_SVC_RELAXED_POLL)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             last = sq;
             // the inline message bytes (up to 1 KiB) into ring slot 0 in the
             // same round trip as the arguments
