@@ -1040,6 +1040,11 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #endif
 // NKFS_BE_RING: the hash waves' load ring, in batches of 8 rounds (RING - 1
 // batches in flight while one is folded)
+// NKFS_BE_DIAG8 (default 1): units of 8 parts (32 < k <= 64) take the
+// diagonal tables whether or not enc_bign 3 pins them
+#ifndef NKFS_BE_DIAG8
+#define NKFS_BE_DIAG8 1
+#endif
 #ifndef NKFS_BE_RING
 #define NKFS_BE_RING 4
 #endif
@@ -1091,7 +1096,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                                                                    u32 ngroups, u32 nunits, u32 *uctr)
 {
     static_assert(P == 16 || (P == 8 && KC == 0), "part groups of 16, or of 8 without contiguous-row loads");
-    static_assert(!DIAG || P == 16, "diagonal tables: units of 16 parts");
+    // DIAG with P = 8: 16-column chunks of 32 KiB (k <= 64, the launcher)
     // HWV hash waves (units go round them), EW encoders
     static_assert(HWV >= 1 && HWV <= 8, "one to eight hash waves");
     constexpr int EW = BE_WAVES - HWV;
@@ -1194,41 +1199,49 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                 xb = r;
             }
             if constexpr (DIAG) {
-                // diagonal layout: entry x of column m at (m >> 4) * 64 KiB +
-                // x * 256 + (m & 15) * 16, so the 16 columns of a chunk sit in
-                // the 16 bank slots of each 256-byte x row.  The rows go
-                // through the LDS; then wave 4c + qt builds x = xl + 4 s + 64
-                // qt of chunk c's 16 tables, lane 16 xl + j its table j:
-                // the 8 lanes of a ds_write_b128 group write 8 bank slots of
-                // one x row (no conflict)
+                // diagonal layout: entry x of column m at (m >> 4) * CB + x *
+                // 16 P + (m & 15) * P (P = 16: 64 KiB chunks, 256-byte x rows;
+                // P = 8: 32 KiB, 128-byte rows), so the 16 columns of a chunk
+                // sit in 16 distinct bank slots of each x row.  The rows go
+                // through the LDS; then job 4c + qt builds x = xl + 4 s + 64
+                // qt of chunk c's 16 tables, lane 16 xl + j its table j: the
+                // lanes of a ds_write group write distinct slots of one x row
                 {
-                    const int t = lane / 16, e = lane % 16, m = wave + EW * t;
+                    const int t = lane / P, e = lane % P, m = wave + EW * t;
                     if (t < TP && m < 16 * nch)
-                        vrow[m * 16 + e] = u8(xb);
+                        vrow[m * P + e] = u8(xb);
                 }
                 enc_barrier<EW>(&bar, gen, lane);
-                if (wave < 4 * nch) {
-                    const int c = wave >> 2, qt = wave & 3, j = lane & 15, xl = lane >> 4;
-                    const uint4 rv = *reinterpret_cast<const uint4 *>(vrow + (16 * c + j) * 16);
-                    const u32 row[4] = {rv.x, rv.y, rv.z, rv.w};
-                    u32 basis[8][4];
-                    make_basis<4>(basis, row);
-                    u32 hv[4];
+                constexpr int W4 = P / 4;
+                constexpr u32 CB = P == 16 ? 65536u : 32768u, XB = 16u * u32(P);
+#pragma unroll 1
+                for (int job = wave; job < 4 * nch; job += EW) {
+                    const int c = job >> 2, qt = job & 3, j = lane & 15, xl = lane >> 4;
+                    u32 row[W4];
 #pragma unroll
-                    for (int w = 0; w < 4; ++w)
+                    for (int w = 0; w < W4; ++w)
+                        row[w] = reinterpret_cast<const u32 *>(vrow + (16 * c + j) * P)[w];
+                    u32 basis[8][W4];
+                    make_basis<W4>(basis, row);
+                    u32 hv[W4];
+#pragma unroll
+                    for (int w = 0; w < W4; ++w)
                         hv[w] = (basis[0][w] & (0u - u32(xl & 1))) ^ (basis[1][w] & (0u - u32(xl >> 1))) ^
                                 (basis[6][w] & (0u - u32(qt & 1))) ^ (basis[7][w] & (0u - u32(qt >> 1)));
-                    u8 *tb = tbl + u32(c) * 65536u + u32(j) * 16u;
+                    u8 *tb = tbl + u32(c) * CB + u32(j) * u32(P);
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         if (i) {
                             const int bit = __builtin_ctz(i);
 #pragma unroll
-                            for (int w = 0; w < 4; ++w)
+                            for (int w = 0; w < W4; ++w)
                                 hv[w] ^= basis[2 + bit][w];
                         }
                         const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 64u * u32(qt);
-                        *reinterpret_cast<uint4 *>(tb + x * 256u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+                        if constexpr (P == 16)
+                            *reinterpret_cast<uint4 *>(tb + x * XB) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+                        else
+                            *reinterpret_cast<uint2 *>(tb + x * XB) = make_uint2(hv[0], hv[1]);
                     }
                 }
             }
@@ -1520,6 +1533,19 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const u32 nsl = (v.ps + ROWS - 1) / ROWS;
             const u32 rl = u32(wave * 64 + lane) * 4u;
             constexpr int NCH = (BE_CMAX8 + 15) / 16;
+            // DIAG: as the P = 16 path, with 8-byte entries at x * 128 + slot
+            // * 8: the slot bytes hold slot * 16 and the address is halved
+            const u32 r16 = u32(lane & 15);
+            const u32 mk2 = (r16 & 8u) ? ~0u : 0u, mk1 = (r16 & 4u) ? ~0u : 0u, rb = r16 & 3u;
+            u32 slot4[4];
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                u32 x = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    x |= (((u32(4 * gq + i) + r16) & 15u) << 4) << (8 * i);
+                slot4[gq] = x;
+            }
             u32 raw[2][4][5];
             auto load = [&](u32 (&x)[4][5], u32 r0, int c) {
 #pragma unroll
@@ -1564,6 +1590,44 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                                 d[q][w] &= u32((u64(1) << (8 * keep)) - 1u);
                             }
                         }
+                    }
+                    if constexpr (DIAG) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            u32 a[4], b[4];
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                a[w] = mux3(mk2, d[q][(w + 2) & 3], d[q][w]);
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                b[w] = mux3(mk1, a[(w + 1) & 3], a[w]);
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                d[q][w] = __builtin_amdgcn_alignbyte(b[(w + 1) & 3], b[w], rb);
+                        }
+                        // every step: columns past k meet zero tables
+                        u32 tdep = u32(c) * 32768u;
+#pragma unroll
+                        for (int j = 0; j < 16; j += 2) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const u32 t0 = 0x0C0C0004u | (u32(j & 3) << 8) | u32(j & 3);
+                                const u32 t1 = 0x0C0C0004u | (u32((j + 1) & 3) << 8) | u32((j + 1) & 3);
+                                const u32 P0 = (__builtin_amdgcn_perm(slot4[j >> 2], d[q][j >> 2], t0) >> 1) + tdep;
+                                const u32 P1 =
+                                    (__builtin_amdgcn_perm(slot4[(j + 1) >> 2], d[q][(j + 1) >> 2], t1) >> 1) + tdep;
+                                const uint2 a = *reinterpret_cast<const uint2 *>(tbl + P0);
+                                const uint2 c2 = *reinterpret_cast<const uint2 *>(tbl + P1);
+                                acc[q].x = xor3(acc[q].x, a.x, c2.x);
+                                acc[q].y = xor3(acc[q].y, a.y, c2.y);
+                            }
+                            if (j & 2) {
+                                u32 z;
+                                asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(acc[3].x));
+                                tdep = u32(c) * 32768u + z;
+                            }
+                        }
+                        continue;
                     }
                     // columns in pairs, the bytes past k meet zero tables
                     u32 tdep = 0;
@@ -1847,6 +1911,10 @@ extern "C" int nkfs_bign_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t
     };
     auto pick = [&](auto hash) {
         if (P == 8) {
+            if (k <= 64 && (diag || NKFS_BE_DIAG8))
+                hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0, true, NKFS_BE_HW>), dim3(grid),
+                                   dim3(64 * BE_WAVES), 0, st, *g, ids, digests, u32(ngroups), u32(nunits), uctr);
+            else
             hipLaunchKernelGGL((k_encode_bign<8, decltype(hash)::value, 0, false, NKFS_BE_HW>), dim3(grid), dim3(64 * BE_WAVES), 0, st,
                                *g, ids, digests, u32(ngroups), u32(nunits), uctr);
             return;
