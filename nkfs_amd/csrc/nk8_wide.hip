@@ -185,6 +185,10 @@ __global__ __launch_bounds__(256) void k_encode_wide(nkfs_geom g, const u8 *ids,
 // PF: chunks of block loads in flight per encoder lane (1: the next chunk's
 // loads issue after this chunk's lookups; 2: two register sets rotate, so
 // a chunk's loads have two chunk periods to arrive).
+// NKFS_WW_HPRIO (experiment builds): the hash wave's s_setprio level
+#ifndef NKFS_WW_HPRIO
+#define NKFS_WW_HPRIO 0
+#endif
 template <int K, int NE, int PF>
 __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g, const u8 *ids, u64 *digests,
                                                                   u32 ngroups)
@@ -324,6 +328,8 @@ __global__ __launch_bounds__(64 * (NE + 1), 2) void k_encode_wide_ws(nkfs_geom g
     }
 
     // ---------------------------------------------------------------- hash wave
+    if (NKFS_WW_HPRIO)
+        __builtin_amdgcn_s_setprio(NKFS_WW_HPRIO);
     const int hi = lane >> 2, ha = lane & 3;  // part p0 + hi, accumulator ha
     const bool hlane = hi < np;
     const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
