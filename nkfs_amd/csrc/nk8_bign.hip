@@ -1040,6 +1040,12 @@ int launch_bigr(const nkfs_geom *g, const uint8_t *work, const int32_t *status, 
 #endif
 // NKFS_BE_RING: the hash waves' load ring, in batches of 8 rounds (RING - 1
 // batches in flight while one is folded)
+// NKFS_BE_LAG (experiment builds, 0 = off): encoder waves stay at most this
+// many slices ahead of the unit's hash wave, so its re-read of the parts
+// hits the XCD's L2 instead of HBM
+#ifndef NKFS_BE_LAG
+#define NKFS_BE_LAG 0
+#endif
 // NKFS_BE_DIAG8 (default 1): units of 8 parts (32 < k <= 64) take the
 // diagonal tables whether or not enc_bign 3 pins them
 #ifndef NKFS_BE_DIAG8
@@ -1113,6 +1119,7 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
     __shared__ u32 bar;
     __shared__ u32 uq[8];           // NKFS_BE_DYN: the workgroup's claimed units, in order
     __shared__ u32 uq_n, hdone;     // claims published / units the hash wave finished
+    __shared__ u32 hseq[8];         // NKFS_BE_LAG: slices each hash wave has folded (or skipped)
     const bool dyn = NKFS_BE_DYN && uctr && HWV == 1;
 
     const int n = g.n, k = g.k;
@@ -1124,6 +1131,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
     const int nch = (kk + 15) >> 4;
     if (tid < BE_WAVES)
         done[tid] = 0;
+    if (tid < 8)
+        hseq[tid] = 0;
     if (tid == 0) {
         bar = 0;
         uq_n = 0;
@@ -1344,6 +1353,14 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
                 const u32 r0 = sl * ROWS + rl;
+                if (HASH && NKFS_BE_LAG && !dyn) {
+                    // at most NKFS_BE_LAG slices ahead of the unit's hash
+                    // wave: its re-read of the parts stays in the XCD's L2
+                    const u32 hw = ci % u32(HWV);
+                    while (__hip_atomic_load(&hseq[hw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                               u32(NKFS_BE_LAG) < seq + 1u)
+                        __builtin_amdgcn_s_sleep(1);
+                }
                 const bool last = sl + 1 == nsl;
                 uint4 acc[4];
 #pragma unroll
@@ -1563,6 +1580,14 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
                 const u32 r0 = sl * ROWS + rl;
+                if (HASH && NKFS_BE_LAG && !dyn) {
+                    // at most NKFS_BE_LAG slices ahead of the unit's hash
+                    // wave: its re-read of the parts stays in the XCD's L2
+                    const u32 hw = ci % u32(HWV);
+                    while (__hip_atomic_load(&hseq[hw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                               u32(NKFS_BE_LAG) < seq + 1u)
+                        __builtin_amdgcn_s_sleep(1);
+                }
                 const bool last = sl + 1 == nsl;
                 uint2 acc[4];
 #pragma unroll
@@ -1726,6 +1751,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             const u32 nsl = (v.ps + ROWS - 1) / ROWS;
             if (HWV > 1 && int(ci % u32(HWV)) != wave - EW) {
                 seq += nsl;  // the other hash wave's unit
+                if (NKFS_BE_LAG && lane == 0)
+                    __hip_atomic_store(&hseq[wave - EW], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 continue;
             }
             const u32 nst = v.ps >> 5;  // whole 32-byte stripes of every part
@@ -1737,6 +1764,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
             u64 hacc = xxh_acc_init(a, 0);
 #pragma unroll 1
             for (u32 sl = 0; sl < nsl; ++sl) {
+                if (NKFS_BE_LAG && lane == 0)  // the slices before this one are folded
+                    __hip_atomic_store(&hseq[wave - EW], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 ++seq;
                 if (!NKFS_BE_PROG) {
                     for (;;) {
@@ -1790,6 +1819,8 @@ __global__ __launch_bounds__(64 * BE_WAVES, 1) void k_encode_bign(nkfs_geom g, c
                     }
                 }
             }
+            if (NKFS_BE_LAG && lane == 0)
+                __hip_atomic_store(&hseq[wave - EW], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             // every slice is stored: the tail (ps & 31 bytes after the last
             // whole stripe), converge, length, avalanche
             uint64_t tw[4] = {0, 0, 0, 0};
