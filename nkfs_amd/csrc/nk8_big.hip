@@ -472,6 +472,226 @@ __global__ __launch_bounds__(256, 2) void k_encode_big(nkfs_geom g, const u8 *id
     }
 }
 
+// k_encode_big without the fused XXH64, in workgroups of 8 waves sharing one
+// chunk table (NKFS_BIG_W8): k_encode_big's 72 KiB of LDS per 4-wave
+// workgroup allow two per CU, 8 waves, and its SQ counters show half of
+// their time waiting (W3: 7.7 waves per CU, 48 % wait,
+// profiles/r06/sq_w3final_summary.txt); here two 8-wave workgroups share the
+// CU's LDS the same way: 16 waves.  Same slice (4,096 rows = 512 lanes x 8),
+// diagonal tables, output through a [part quad][512 rows] stage.  W3 1,001
+// -> 1,135 GB/s, N40K33 1,074 -> 1,275, N80K70 850 -> 959 (with the XXH64
+// pass; profiles/r06/ab_big8.txt)
+#ifndef NKFS_BIG_W8
+#define NKFS_BIG_W8 1
+#endif
+constexpr int ENC8_T = 8;  // rows per lane per slice (512 lanes: ENC_ROWS rows)
+static_assert(512 * ENC8_T == int(ENC_ROWS), "same slice as k_encode_big");
+
+__global__ __launch_bounds__(512, 4) void k_encode_big8(nkfs_geom g, const u8 *ids, const GfTables *gft,
+                                                        u32 ngroups, u32 nslices)
+{
+    __shared__ __attribute__((aligned(16))) u8 tbl[16 * 256 * 16];   // 16 diagonal tables
+    __shared__ __attribute__((aligned(16))) u32 stage[4 * 512];      // [part quad][row]
+    __shared__ __attribute__((aligned(16))) uint4 coef[256];
+    __shared__ uint16_t glog[256];
+    __shared__ u8 gexp[256];
+
+    const u32 b = blockIdx.x;
+    const u32 loc = b >> 3;
+    const u32 noct = (g.nstripes + 7) / 8;
+    const u32 grp = loc % ngroups;
+    const u32 slice = loc / (ngroups * noct);
+    const u32 s = ((loc / ngroups) % noct) * 8 + (b & 7);
+    if (s >= g.nstripes || slice >= nslices)
+        return;  // the whole workgroup
+    const Stripe v = stripe_at(g, s);
+    const u32 r_begin = slice * ENC_ROWS;
+    if (r_begin >= v.ps)
+        return;
+    const int n = g.n, k = g.k;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int p0 = int(grp) * 16, np = min(16, n - p0);
+
+    if (tid < 256) {
+        glog[tid] = gft->log[tid];
+        gexp[tid] = gft->exp[tid];
+    }
+    __syncthreads();
+    {
+        const u8 *sid = ids + u64(s) * u64(n) + p0;
+        u32 xs[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            xs[e] = e < np ? sid[e] : 0u;
+        for (int m = tid; m < k; m += 512) {
+            u32 w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                if (e < np)
+                    w[e >> 2] |= gf_pow(glog, gexp, xs[e], u32(m)) << (8 * (e & 3));
+            coef[m] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+    const u32 mis = u32(reinterpret_cast<uintptr_t>(v.blk) & 3u);
+    const __amdgpu_buffer_rsrc_t rs = brsrc(v.blk - mis, (v.B + mis + 3u) & ~3u);
+    uint4 acc[ENC8_T];
+#pragma unroll
+    for (int t = 0; t < ENC8_T; ++t)
+        acc[t] = make_uint4(0, 0, 0, 0);
+    const u32 r16 = u32(lane & 15);
+    const u32 mk8 = (r16 & 8u) ? ~0u : 0u, mk4 = (r16 & 4u) ? ~0u : 0u, rb3 = r16 & 3u;
+    u32 dslot[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+        u32 x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            x |= (((u32(4 * gq + i) + r16) & 15u) << 4) << (8 * i);
+        dslot[gq] = x;
+    }
+    const int nch = (k + 15) / 16;
+    for (int cc = 0; cc < nch; ++cc) {
+        __syncthreads();  // coef[] written / the previous chunk's lookups done
+        {
+            // lane l of wave w builds table j = l & 15, entries x = (l >> 4)
+            // + 4 i + 32 w (Gray-code walk over i < 8)
+            const int j = lane & 15, xl = lane >> 4, m = 16 * cc + j;
+            const uint4 c = m < k ? coef[m] : make_uint4(0, 0, 0, 0);
+            const u32 row[4] = {c.x, c.y, c.z, c.w};
+            u32 basis[8][4];
+            make_basis<4>(basis, row);
+            u32 hv[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                u32 e = 0;
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb)
+                    e ^= basis[bb][w] & (0u - ((u32(xl) >> bb) & 1u));
+#pragma unroll
+                for (int bb = 0; bb < 3; ++bb)
+                    e ^= basis[5 + bb][w] & (0u - ((u32(wave) >> bb) & 1u));
+                hv[w] = e;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i) {
+                    const int bit = __builtin_ctz(i);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        hv[w] ^= basis[2 + bit][w];
+                }
+                const u32 x = u32(xl) + 4u * u32(i ^ (i >> 1)) + 32u * u32(wave);
+                *reinterpret_cast<uint4 *>(tbl + x * 256u + u32(j) * 16u) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            }
+        }
+        __syncthreads();
+        const bool tail = (u64(r_begin) + ENC_ROWS) * u64(k) > u64(v.B);
+        auto rows = [&](auto mask) {
+            constexpr bool MASK = decltype(mask)::value;
+            u32 tdep = 0;
+            auto load = [&](int t, v4u &x, u32 &x4, u32 &pos) {
+                const u32 r = r_begin + u32(t) * 512u + u32(tid);
+                pos = r * u32(k) + 16u * u32(cc);
+                const u32 a = (pos + mis + tdep) & ~3u;
+                x = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+                x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, a + 16u, 0, 0);
+            };
+            v4u xc, xn;
+            u32 x4c, x4n, posc, posn;
+            load(0, xc, x4c, posc);
+#pragma unroll
+            for (int t = 0; t < ENC8_T; ++t) {
+                if (t + 1 < ENC8_T)
+                    load(t + 1, xn, x4n, posn);
+                const u32 sh = (posc + mis) & 3u;
+                u32 d[4];
+                d[0] = __builtin_amdgcn_alignbyte(xc.y, xc.x, sh);
+                d[1] = __builtin_amdgcn_alignbyte(xc.z, xc.y, sh);
+                d[2] = __builtin_amdgcn_alignbyte(xc.w, xc.z, sh);
+                d[3] = __builtin_amdgcn_alignbyte(x4c, xc.w, sh);
+                if constexpr (MASK) {
+                    const u32 valid = v.B > posc ? min(v.B - posc, 16u) : 0u;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const u32 keep = valid > u32(4 * w) ? min(valid - u32(4 * w), 4u) : 0u;
+                        d[w] &= u32((u64(1) << (8 * keep)) - 1u);
+                    }
+                }
+                u32 a[4], b2[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    a[w] = big_mux(mk8, d[(w + 2) & 3], d[w]);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    b2[w] = big_mux(mk4, a[(w + 1) & 3], a[w]);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    d[w] = __builtin_amdgcn_alignbyte(b2[(w + 1) & 3], b2[w], rb3);
+                uint4 e = acc[t];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (j == 8) {  // eight lookups in flight at most (128 VGPRs)
+                        u32 z;
+                        asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(e.x));
+                        tdep += z;
+                    }
+                    const u32 sel = 0x0C0C0004u | (u32(j & 3) << 8) | u32(j & 3);
+                    const u32 P = __builtin_amdgcn_perm(dslot[j >> 2], d[j >> 2], sel) + tdep;
+                    const uint4 tv = *reinterpret_cast<const uint4 *>(tbl + P);
+                    e.x ^= tv.x;
+                    e.y ^= tv.y;
+                    e.z ^= tv.z;
+                    e.w ^= tv.w;
+                }
+                acc[t] = e;
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(tdep) : "v"(e.x), "v"(e.y), "v"(e.z), "v"(e.w));
+                xc = xn;
+                x4c = x4n;
+                posc = posn;
+            }
+        };
+        if (tail)
+            rows(std::true_type{});
+        else
+            rows(std::false_type{});
+    }
+
+    // 512 rows x 16 parts per t-unit: [part quad][row] in LDS, read back as 4
+    // rows x 4 parts, 4x4 byte transpose: wave w stores part quad w & 3 of
+    // rows (w >> 2) * 256 .., 256 contiguous bytes of a part per instruction
+    const bool pal = ((reinterpret_cast<uintptr_t>(v.parts) | v.pitch) & 3) == 0;
+    const int pq = wave & 3, half = wave >> 2;
+#pragma unroll
+    for (int t = 0; t < ENC8_T; ++t) {
+        const u32 rt = r_begin + u32(t) * 512u;
+        if (rt >= v.ps)
+            break;  // workgroup-uniform
+        __syncthreads();
+        stage[0 * 512 + tid] = acc[t].x;
+        stage[1 * 512 + tid] = acc[t].y;
+        stage[2 * 512 + tid] = acc[t].z;
+        stage[3 * 512 + tid] = acc[t].w;
+        __syncthreads();
+        const uint4 q4 = *reinterpret_cast<const uint4 *>(stage + pq * 512 + half * 256 + 4 * lane);
+        u32 o[4];
+        transpose4(q4.x, q4.y, q4.z, q4.w, o[0], o[1], o[2], o[3]);
+        const u32 rr = rt + u32(half) * 256u + 4u * u32(lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * pq + j;
+            if (e < np && rr < v.ps) {
+                u8 *dst = v.parts + u64(p0 + e) * v.pitch + rr;
+                if (pal && rr + 4u <= v.ps) {
+                    *reinterpret_cast<u32 *>(dst) = o[j];
+                } else {
+                    for (u32 c = 0; c < 4 && rr + c < v.ps; ++c)
+                        dst[c] = u8(o[j] >> (8 * c));
+                }
+            }
+        }
+    }
+}
+
 // The fused hash's safety net: when a chain wait timed out (ch.fail; not
 // expected -- slice i-1 is dispatched long before slice i on the same XCD),
 // every part's digest is recomputed here, four lanes per part; otherwise
@@ -725,8 +945,13 @@ extern "C" int nkfs_big_encode(const nkfs_geom *g, const uint8_t *ids, uint64_t 
     if (grid > 0x7FFFFFFFull)
         return -EINVAL;
     if (!digests) {
-        hipLaunchKernelGGL(k_encode_big<false>, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
-                           u32(ngroups), u32(nslices ? nslices : 1), BigChain{});
+        constexpr bool w8 = NKFS_BIG_W8 != 0 && NKFS_BIG_DIAG != 0;
+        if (w8)
+            hipLaunchKernelGGL(k_encode_big8, dim3(u32(grid)), dim3(512), 0, st, *g, ids, (const GfTables *)gf,
+                               u32(ngroups), u32(nslices ? nslices : 1));
+        else
+            hipLaunchKernelGGL(k_encode_big<false>, dim3(u32(grid)), dim3(256), 0, st, *g, ids, (const GfTables *)gf,
+                               u32(ngroups), u32(nslices ? nslices : 1), BigChain{});
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
     // hand-off records: per (stripe, group) 64 accumulators + a flag, and the failure word
